@@ -1,0 +1,39 @@
+# Build recipe for every native artefact (no cmake/ninja needed).
+#   libfdf.so        HIP kernels + C ABI (the product), gfx950 only
+#   liboracle.so     scalar C restatement of the reference semantics (test infrastructure)
+#   libfast_avx2.so  C++ AVX2 port of the reference's fast_simd path (CPU baseline only)
+#   test_cpp_api     C++ API (include/fdf.hpp) smoke binary
+HIPCC ?= /opt/rocm/bin/hipcc
+CC ?= gcc
+CXX ?= g++
+ARCH ?= gfx950
+
+PKG := feature_detector_fast_amd
+CSRC := $(PKG)/csrc
+LIBFDF := $(PKG)/libfdf.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude
+
+all: $(LIBFDF) oracle/liboracle.so oracle/libfast_avx2.so tests/cpp/test_cpp_api
+
+$(CSRC)/fdf_kernels.o: $(CSRC)/fdf_kernels.hip $(CSRC)/fdf_kernels.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/fdf_api.o: $(CSRC)/fdf_api.cpp $(CSRC)/fdf_kernels.h include/fdf.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+oracle/liboracle.so: oracle/fast_oracle.c oracle/fast_oracle.h
+	$(CC) -O2 -std=c11 -fPIC -shared -Wall -o $@ $<
+
+oracle/libfast_avx2.so: oracle/fast_avx2.cpp
+	$(CXX) -O3 -mavx2 -std=c++17 -fPIC -shared -Wall -o $@ $< -lpthread
+
+tests/cpp/test_cpp_api: tests/cpp/test_cpp_api.cpp include/fdf.hpp include/fdf.h $(LIBFDF)
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG) -lfdf -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+
+clean:
+	rm -f $(CSRC)/*.o $(LIBFDF) oracle/*.so tests/cpp/test_cpp_api
+
+.PHONY: all clean

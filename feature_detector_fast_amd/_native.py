@@ -1,0 +1,144 @@
+"""ctypes binding of the C ABI in include/fdf.h (libfdf.so, built in-tree by ``make``).
+
+There is no fallback: if the shared library is missing or no HIP device is visible the
+calls raise :class:`FdfError` -- the HIP kernels are the only implementation.
+"""
+import ctypes
+import importlib.util
+import os
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfdf.so")
+
+# include/fdf.h enum fdf_status
+FDF_OK = 0
+FDF_ERR_COUNT = 1
+FDF_ERR_SIZE = 2
+FDF_ERR_CAPACITY = 3
+FDF_ERR_NMS = 4
+FDF_ERR_DEVICE = 5
+FDF_ERR_ARG = 6
+FDF_ERR_ALLOC = 7
+
+# Every symbol include/fdf.h declares (tests/test_abi.py checks the .so exports them all).
+EXPORTED_SYMBOLS = (
+    "fdf_abi_version", "fdf_status_string", "fdf_device_count", "fdf_validate",
+    "fdf_ctx_create", "fdf_ctx_destroy", "fdf_ctx_stream", "fdf_detect", "fdf_detect_batch",
+    "fdf_detect_device", "fdf_score_points",
+)
+
+
+class FdfConfig(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_uint8), ("count", ctypes.c_uint8), ("nms", ctypes.c_uint8)]
+
+
+class FdfPoint(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint32), ("y", ctypes.c_uint32)]
+
+
+class FdfError(RuntimeError):
+    """A non-OK fdf_status; ``.status`` holds the code."""
+
+    def __init__(self, status, where=""):
+        self.status = status
+        msg = status_string(status) if _lib is not None else f"status {status}"
+        super().__init__(f"{where}: {msg}" if where else msg)
+
+
+_lib = None
+
+
+def _share_torch_runtime():
+    """Map PyTorch's bundled HIP runtime before libfdf.so when torch is installed.
+
+    torch ships its own libamdhip64.so (SONAME libamdhip64.so.7).  If libfdf.so were loaded
+    first it would map /opt/rocm's copy, and a later ``import torch`` would map a second HIP
+    runtime into the process, which then fails to initialise.  With torch's copy mapped
+    first, libfdf.so's NEEDED libamdhip64.so.7 binds to it, so device pointers and streams
+    are shared with torch.  Without torch, /opt/rocm's runtime is used."""
+    if "torch" in sys.modules:
+        return
+    spec = importlib.util.find_spec("torch")
+    if spec is None or spec.origin is None:
+        return
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def load():
+    """Load libfdf.so once and declare the prototypes.  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FdfError(FDF_ERR_DEVICE, f"{LIB_PATH} is not built (run `make` or __graft_entry__.build())")
+    _share_torch_runtime()
+    lib = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    vp = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    u32 = ctypes.c_uint32
+    u64 = ctypes.c_uint64
+    cfgp = ctypes.POINTER(FdfConfig)
+    lib.fdf_abi_version.restype = ctypes.c_int
+    lib.fdf_status_string.restype = ctypes.c_char_p
+    lib.fdf_status_string.argtypes = [ctypes.c_int]
+    lib.fdf_device_count.restype = ctypes.c_int
+    lib.fdf_validate.restype = ctypes.c_int
+    lib.fdf_validate.argtypes = [u32, u32, cfgp, ctypes.POINTER(ctypes.c_int)]
+    lib.fdf_ctx_create.restype = ctypes.c_int
+    lib.fdf_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    lib.fdf_ctx_destroy.restype = None
+    lib.fdf_ctx_destroy.argtypes = [vp]
+    lib.fdf_ctx_stream.restype = vp
+    lib.fdf_ctx_stream.argtypes = [vp]
+    lib.fdf_detect.restype = ctypes.c_int
+    lib.fdf_detect.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, ctypes.POINTER(sz)]
+    lib.fdf_detect_batch.restype = ctypes.c_int
+    lib.fdf_detect_batch.argtypes = [vp, vp, u32, u32, u32, sz, cfgp, vp, sz, vp,
+                                     ctypes.POINTER(sz)]
+    lib.fdf_detect_device.restype = ctypes.c_int
+    lib.fdf_detect_device.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp]
+    lib.fdf_score_points.restype = ctypes.c_int
+    lib.fdf_score_points.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, vp]
+    del u8p
+    _lib = lib
+    return lib
+
+
+def status_string(status):
+    return load().fdf_status_string(int(status)).decode()
+
+
+def check(status, where=""):
+    if status != FDF_OK:
+        raise FdfError(status, where)
+
+
+class Context:
+    """One device + one HIP stream (fdf_ctx_create / fdf_ctx_destroy)."""
+
+    def __init__(self, device=0):
+        lib = load()
+        handle = ctypes.c_void_p()
+        check(lib.fdf_ctx_create(int(device), ctypes.byref(handle)), "fdf_ctx_create")
+        self._lib = lib
+        self.handle = handle
+        self.device = int(device)
+
+    @property
+    def stream(self):
+        return self._lib.fdf_ctx_stream(self.handle)
+
+    def close(self):
+        if self.handle:
+            self._lib.fdf_ctx_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,341 @@
+// fdf_api.cpp -- the C ABI of include/fdf.h on top of the HIP kernels.
+//
+// Replaces fast_simd::detector (iwanders/feature_detector_fast src/fast_simd.rs:847-859):
+// validation mirrors the reference's panics (:302-305, :342, :369, :800) as status codes,
+// the device work is the fused band kernel (fdf_kernels.hip), and the host side only moves
+// bytes and picks the band height.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "../../include/fdf.h"
+#include "fdf_kernels.h"
+
+struct fdf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // device workspace, grown on demand
+    uint8_t* d_in = nullptr;            size_t in_bytes = 0;
+    uint2* d_out = nullptr;             size_t out_points = 0;
+    uint64_t* d_offsets = nullptr;      size_t offsets_n = 0;
+    unsigned long long* d_state = nullptr; size_t state_n = 0;
+    uint32_t* d_counter = nullptr;
+    uint32_t epoch = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int check_config(const fdf_config* cfg) {
+    if (!cfg) return FDF_ERR_ARG;
+    if (cfg->count < 9 || cfg->count > 16) return FDF_ERR_COUNT;
+    if (cfg->nms > FDF_NMS_SUM_ABSOLUTE) return FDF_ERR_NMS;
+    return FDF_OK;
+}
+
+// Shape rules derived from the reference's u32 arithmetic (SURVEY.md §7 "Errors").
+int check_shape(uint32_t w, uint32_t h, int* empty) {
+    *empty = 0;
+    if (h < 3) return FDF_ERR_SIZE;        // height - 3 underflows (src/fast_simd.rs:342)
+    if (h <= 6) { *empty = 1; return FDF_OK; }
+    if (w < 6) return FDF_ERR_SIZE;        // width - 3 - 3 underflows (:369)
+    if (w == 6) { *empty = 1; return FDF_OK; }
+    return FDF_OK;
+}
+
+template <typename T>
+int ensure(T** buf, size_t* have, size_t need, bool zero, hipStream_t stream) {
+    if (*have >= need) return FDF_OK;
+    if (*buf) { (void)hipStreamSynchronize(stream); (void)hipFree(*buf); *buf = nullptr; *have = 0; }
+    size_t n = std::max(need, *have * 2);
+    if (hipMalloc(reinterpret_cast<void**>(buf), n * sizeof(T)) != hipSuccess) {
+        *buf = nullptr;
+        return FDF_ERR_ALLOC;
+    }
+    if (zero && hipMemsetAsync(*buf, 0, n * sizeof(T), stream) != hipSuccess) return FDF_ERR_DEVICE;
+    *have = n;
+    return FDF_OK;
+}
+
+// Band height: tall bands amortise the 8-row halo; short bands fill the 256 CUs when the
+// whole job is small (e.g. one frame).  Capped so the LDS layout fits.
+uint32_t pick_rows(uint32_t n_frames, uint32_t w, uint32_t h, bool nms) {
+    const uint32_t centre_rows = h - 6;
+    const uint32_t nw = (w + 31) / 32;
+    uint32_t R = 8;
+    if ((uint64_t)n_frames * ((centre_rows + 7) / 8) < 1024) R = 4;
+    while (R > 1 && fdfk::make_layout(R, nw, nms).total > fdfk::kMaxLds) --R;
+    return R;
+}
+
+// Enqueue the band kernel over `n_frames` device frames.  Frames must be valid (w, h >= 7).
+int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
+            uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
+            uint64_t* d_offsets, hipStream_t stream) {
+    const bool nms = cfg->nms != FDF_NMS_OFF;
+    const uint32_t R = pick_rows(n_frames, w, h, nms);
+    const uint32_t nw = (w + 31) / 32;
+    if (fdfk::make_layout(R, nw, nms).total > fdfk::kMaxLds) return FDF_ERR_SIZE;
+    const uint32_t bands = (h - 6 + R - 1) / R;
+    const uint64_t ntasks = (uint64_t)bands * n_frames;
+    if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
+    int rc = ensure(&ctx->d_state, &ctx->state_n, (size_t)ntasks, true, stream);
+    if (rc) return rc;
+    if (!ctx->d_counter) {
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->d_counter), sizeof(uint32_t)) != hipSuccess)
+            return FDF_ERR_ALLOC;
+        if (hipMemsetAsync(ctx->d_counter, 0, sizeof(uint32_t), stream) != hipSuccess)
+            return FDF_ERR_DEVICE;
+    }
+    if (++ctx->epoch > 0xffffu) {   // generation tag wrapped: clear stale look-back words
+        ctx->epoch = 1;
+        if (hipMemsetAsync(ctx->d_state, 0, ctx->state_n * sizeof(unsigned long long), stream) !=
+            hipSuccess)
+            return FDF_ERR_DEVICE;
+    }
+    fdfk::BandParams p;
+    p.frames = d_frames;
+    p.frame_stride = frame_stride;
+    p.width = w;
+    p.height = h;
+    p.rows = R;
+    p.bands_per_frame = bands;
+    p.ntasks = (uint32_t)ntasks;
+    p.words_per_row = nw;
+    p.threshold = cfg->threshold;
+    p.epoch = ctx->epoch;
+    p.out = d_out;
+    p.cap = cap;
+    p.frame_offsets = d_offsets;
+    p.band_state = ctx->d_state;
+    p.task_counter = ctx->d_counter;
+    const char* dbg = std::getenv("FDF_DEBUG_FLAGS");   // ablation builds only, see fdf_kernels.h
+    p.flags = dbg ? (uint32_t)std::strtoul(dbg, nullptr, 0) : 0u;
+    if (fdfk::launch_band_kernel(p, cfg->nms, cfg->count, stream) != hipSuccess)
+        return FDF_ERR_DEVICE;
+    return FDF_OK;
+}
+
+// Shared body of fdf_detect / fdf_detect_batch: host frames in, host points out.
+int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
+                size_t row_stride, size_t frame_stride, const fdf_config* cfg, fdf_point* out,
+                size_t cap, uint64_t* frame_offsets, size_t* n_out) {
+    if (!ctx || !n_out || (cap && !out)) return FDF_ERR_ARG;
+    int rc = check_config(cfg);
+    if (rc) return rc;
+    int empty = 0;
+    rc = check_shape(w, h, &empty);
+    if (rc) return rc;
+    if (n_frames == 0) empty = 1;
+    if (!data && !empty) return FDF_ERR_ARG;
+    if (row_stride < w) return FDF_ERR_ARG;
+    if (empty) {
+        *n_out = 0;
+        if (frame_offsets) std::memset(frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull));
+        return FDF_OK;
+    }
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    const size_t frame_bytes = (size_t)w * h;
+    const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
+    if ((rc = ensure(&ctx->d_in, &ctx->in_bytes, frame_bytes * n_frames, false, ctx->stream))) return rc;
+    if ((rc = ensure(&ctx->d_out, &ctx->out_points, max_points, false, ctx->stream))) return rc;
+    if ((rc = ensure(&ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, false, ctx->stream))) return rc;
+    for (uint32_t f = 0; f < n_frames; ++f) {
+        const uint8_t* src = data + (size_t)f * frame_stride;
+        uint8_t* dst = ctx->d_in + (size_t)f * frame_bytes;
+        hipError_t e = row_stride == w
+                           ? hipMemcpyAsync(dst, src, frame_bytes, hipMemcpyHostToDevice, ctx->stream)
+                           : hipMemcpy2DAsync(dst, w, src, row_stride, w, h, hipMemcpyHostToDevice,
+                                              ctx->stream);
+        if (e != hipSuccess) return FDF_ERR_DEVICE;
+    }
+    rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, ctx->d_out, max_points,
+                 ctx->d_offsets, ctx->stream);
+    if (rc) return rc;
+    uint64_t* offs = frame_offsets;
+    uint64_t local[2];
+    if (!offs) offs = n_frames == 1 ? local : new (std::nothrow) uint64_t[n_frames + 1ull];
+    if (!offs) return FDF_ERR_ALLOC;
+    hipError_t e = hipMemcpyAsync(offs, ctx->d_offsets, sizeof(uint64_t) * (n_frames + 1ull),
+                                  hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    const uint64_t total = offs[n_frames];
+    if (offs != frame_offsets && offs != local) delete[] offs;
+    if (e != hipSuccess) return FDF_ERR_DEVICE;
+    const size_t ncopy = (size_t)std::min<uint64_t>(total, cap);
+    if (ncopy) {
+        e = hipMemcpyAsync(out, ctx->d_out, ncopy * sizeof(fdf_point), hipMemcpyDeviceToHost,
+                           ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return FDF_ERR_DEVICE;
+    }
+    *n_out = (size_t)total;
+    return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fdf_abi_version(void) { return FDF_ABI_VERSION; }
+
+const char* fdf_status_string(int status) {
+    switch (status) {
+        case FDF_OK: return "ok";
+        case FDF_ERR_COUNT: return "count must be in [9, 16]";
+        case FDF_ERR_SIZE: return "image size not supported by the reference (h < 3, or w < 6 with h >= 7)";
+        case FDF_ERR_CAPACITY: return "output buffer too small";
+        case FDF_ERR_NMS: return "unknown non-maximal suppression mode";
+        case FDF_ERR_DEVICE: return "HIP device error";
+        case FDF_ERR_ARG: return "invalid argument";
+        case FDF_ERR_ALLOC: return "allocation failed";
+        default: return "unknown status";
+    }
+}
+
+int fdf_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int fdf_validate(uint32_t width, uint32_t height, const fdf_config* cfg, int* empty) {
+    if (!empty) return FDF_ERR_ARG;
+    int rc = check_config(cfg);
+    if (rc) return rc;
+    return check_shape(width, height, empty);
+}
+
+int fdf_ctx_create(int device, fdf_ctx** out_ctx) {
+    if (!out_ctx) return FDF_ERR_ARG;
+    *out_ctx = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return FDF_ERR_DEVICE;
+    fdf_ctx* ctx = new (std::nothrow) fdf_ctx();
+    if (!ctx) return FDF_ERR_ALLOC;
+    ctx->device = device;
+    DeviceGuard guard(device);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return FDF_ERR_DEVICE;
+    }
+    *out_ctx = ctx;
+    return FDF_OK;
+}
+
+void fdf_ctx_destroy(fdf_ctx* ctx) {
+    if (!ctx) return;
+    {
+        DeviceGuard guard(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->d_in);
+        (void)hipFree(ctx->d_out);
+        (void)hipFree(ctx->d_offsets);
+        (void)hipFree(ctx->d_state);
+        (void)hipFree(ctx->d_counter);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+void* fdf_ctx_stream(fdf_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+               size_t stride_bytes, const fdf_config* cfg, fdf_point* out, size_t cap,
+               size_t* n_out) {
+    return detect_host(ctx, data, 1, width, height, stride_bytes, 0, cfg, out, cap, nullptr,
+                       n_out);
+}
+
+int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t width,
+                     uint32_t height, size_t frame_stride_bytes, const fdf_config* cfg,
+                     fdf_point* out, size_t cap, uint64_t* frame_offsets, size_t* n_out) {
+    if (n_frames > 1 && frame_stride_bytes < (size_t)width * height) return FDF_ERR_ARG;
+    return detect_host(ctx, data, n_frames, width, height, width, frame_stride_bytes, cfg, out,
+                       cap, frame_offsets, n_out);
+}
+
+int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
+                      uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
+                      const fdf_config* cfg, fdf_point* d_out, uint64_t cap,
+                      uint64_t* d_frame_offsets, void* stream) {
+    if (!ctx || !d_frame_offsets) return FDF_ERR_ARG;
+    int rc = check_config(cfg);
+    if (rc) return rc;
+    int empty = 0;
+    rc = check_shape(width, height, &empty);
+    if (rc) return rc;
+    if (n_frames == 0) empty = 1;
+    if (!empty && (!d_frames || (cap && !d_out))) return FDF_ERR_ARG;
+    if (n_frames > 1 && frame_stride_bytes < (uint64_t)width * height) return FDF_ERR_ARG;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);   // NULL = the HIP null stream
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    if (empty) {
+        return hipMemsetAsync(d_frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull), s) ==
+                       hipSuccess
+                   ? FDF_OK
+                   : FDF_ERR_DEVICE;
+    }
+    return enqueue(ctx, d_frames, n_frames, width, height,
+                   n_frames > 1 ? frame_stride_bytes : (uint64_t)width * height, cfg,
+                   reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s);
+}
+
+int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+                     size_t stride_bytes, const fdf_config* cfg, const fdf_point* points,
+                     size_t n_points, uint16_t* out_scores) {
+    if (!ctx || !cfg || (n_points && (!points || !out_scores || !data))) return FDF_ERR_ARG;
+    if (cfg->count < 9 || cfg->count > 16) return FDF_ERR_COUNT;
+    if (cfg->nms != FDF_NMS_MAX_THRESHOLD && cfg->nms != FDF_NMS_SUM_ABSOLUTE) return FDF_ERR_NMS;
+    if (stride_bytes < width || n_points > 0xffffffffull) return FDF_ERR_ARG;
+    for (size_t k = 0; k < n_points; ++k) {
+        const fdf_point p = points[k];
+        if (p.x < 3 || p.y < 3 || (uint64_t)p.x + 3 >= width || (uint64_t)p.y + 3 >= height)
+            return FDF_ERR_ARG;
+    }
+    if (n_points == 0) return FDF_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    const size_t frame_bytes = (size_t)width * height;
+    int rc;
+    if ((rc = ensure(&ctx->d_in, &ctx->in_bytes, frame_bytes, false, ctx->stream))) return rc;
+    if ((rc = ensure(&ctx->d_out, &ctx->out_points, n_points + (n_points + 3) / 4, false,
+                     ctx->stream)))
+        return rc;
+    hipError_t e = stride_bytes == width
+                       ? hipMemcpyAsync(ctx->d_in, data, frame_bytes, hipMemcpyHostToDevice, ctx->stream)
+                       : hipMemcpy2DAsync(ctx->d_in, width, data, stride_bytes, width, height,
+                                          hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->d_out, points, n_points * sizeof(fdf_point), hipMemcpyHostToDevice,
+                           ctx->stream);
+    uint16_t* d_scores = reinterpret_cast<uint16_t*>(ctx->d_out + n_points);
+    if (e == hipSuccess)
+        e = fdfk::launch_score_points(ctx->d_in, width, ctx->d_out, (uint32_t)n_points, cfg->nms,
+                                      cfg->threshold, cfg->count, d_scores, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(out_scores, d_scores, n_points * sizeof(uint16_t), hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
+}
+
+}  // extern "C"

@@ -1,0 +1,174 @@
+"""The HIP detector: drop-in for the reference's ``fast_simd`` module (src/fast_simd.rs).
+
+``detector(img, config)`` replaces ``fast_simd::detector`` (src/fast_simd.rs:847-859) and
+returns ``list[Point]`` in raster order.  Array and batched variants return numpy arrays;
+``detect_device`` keeps everything in HBM (torch CUDA tensors) for throughput.
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _native
+from ._native import FdfConfig, FdfError, check
+from .types import Config, GrayImage, NonMaximalSuppression, Point
+
+# src/fast_simd.rs:69-72
+NORTH = 0
+EAST = 4
+SOUTH = 8
+WEST = 12
+
+_CIRCLE = ((0, -3), (1, -3), (2, -2), (3, -1), (3, 0), (3, 1), (2, 2), (1, 3),
+           (0, 3), (-1, 3), (-2, 2), (-3, 1), (-3, 0), (-3, -1), (-2, -2), (-1, -3))
+
+
+def circle():
+    """The 16-pixel Bresenham circle, index 0 north then clockwise (src/fast_simd.rs:79-98)."""
+    return list(_CIRCLE)
+
+
+def calculate_offsets(width):
+    """Row-major memory offsets of the circle points (src/fast_simd.rs:104-110)."""
+    return [dy * int(width) + dx for dx, dy in _CIRCLE]
+
+
+_ctx_lock = threading.Lock()
+_contexts = {}
+
+
+def context(device=0):
+    """The process-wide :class:`_native.Context` for ``device`` (created on first use)."""
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = _native.Context(device)
+            _contexts[device] = ctx
+        return ctx
+
+
+def _to_c_config(config):
+    if not isinstance(config, Config):
+        raise TypeError("config must be a feature_detector_fast_amd.Config")
+    for name, v in (("threshold", config.threshold), ("count", config.count)):
+        if not 0 <= int(v) <= 255:
+            raise ValueError(f"{name} must fit in u8")
+    nms = int(config.non_maximal_supression)
+    if not 0 <= nms <= 255:
+        raise FdfError(_native.FDF_ERR_NMS, "config")
+    return FdfConfig(int(config.threshold), int(config.count), nms)
+
+
+def _as_pixels(img):
+    if isinstance(img, GrayImage):
+        arr = img.array()
+    else:
+        arr = np.asarray(img)
+    if arr.ndim != 2:
+        raise ValueError("expected a 2-D grayscale image (H, W)")
+    if arr.dtype != np.uint8:
+        raise TypeError("expected uint8 pixels")
+    if arr.strides[1] != 1:
+        arr = np.ascontiguousarray(arr)
+    return arr
+
+
+def detect_array(img, config, device=0):
+    """Keypoints as a (K, 2) uint32 array of (x, y) rows in raster order."""
+    arr = _as_pixels(img)
+    cfg = _to_c_config(config)
+    h, w = arr.shape
+    ctx = context(device)
+    lib = _native.load()
+    n = ctypes.c_size_t(0)
+    stride = arr.strides[0] if arr.size else w
+    ptr = arr.ctypes.data if arr.size else None
+    rc = lib.fdf_detect(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), None, 0, ctypes.byref(n))
+    if rc == _native.FDF_ERR_CAPACITY:
+        out = np.empty((n.value, 2), dtype=np.uint32)
+        rc = lib.fdf_detect(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), out.ctypes.data,
+                            out.shape[0], ctypes.byref(n))
+        check(rc, "fdf_detect")
+        return out[: n.value]
+    check(rc, "fdf_detect")
+    return np.empty((0, 2), dtype=np.uint32)
+
+
+def detector(img, config):
+    """Drop-in for fast_simd::detector: ``list[Point]`` in raster order."""
+    return [Point(int(x), int(y)) for x, y in detect_array(img, config)]
+
+
+def detector_batch(frames, config, device=0):
+    """Detect on a (F, H, W) uint8 stack.  Returns (points (K, 2) uint32, offsets (F+1,))
+    where frame f's keypoints are points[offsets[f]:offsets[f+1]]."""
+    frames = np.ascontiguousarray(np.asarray(frames), dtype=np.uint8)
+    if frames.ndim != 3:
+        raise ValueError("expected a (F, H, W) uint8 stack")
+    f, h, w = frames.shape
+    cfg = _to_c_config(config)
+    ctx = context(device)
+    lib = _native.load()
+    offsets = np.zeros(f + 1, dtype=np.uint64)
+    n = ctypes.c_size_t(0)
+    ptr = frames.ctypes.data if frames.size else None
+    rc = lib.fdf_detect_batch(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg), None, 0,
+                              offsets.ctypes.data, ctypes.byref(n))
+    out = np.empty((0, 2), dtype=np.uint32)
+    if rc == _native.FDF_ERR_CAPACITY:
+        out = np.empty((n.value, 2), dtype=np.uint32)
+        rc = lib.fdf_detect_batch(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg),
+                                  out.ctypes.data, out.shape[0], offsets.ctypes.data,
+                                  ctypes.byref(n))
+    check(rc, "fdf_detect_batch")
+    return out[: n.value], offsets
+
+
+def detect_device(frames, config, out, offsets, stream=None, device=None):
+    """Enqueue detection on device-resident frames; nothing crosses PCIe.
+
+    ``frames``: torch uint8 CUDA tensor (F, H, W), contiguous.  ``out``: int32/uint32 CUDA
+    tensor (cap, 2).  ``offsets``: int64 CUDA tensor (F+1,).  Asynchronous on ``stream``
+    (a torch.cuda.Stream; default: torch's current stream).  On completion
+    offsets[F] holds the total (even when it exceeds ``cap``)."""
+    import torch
+
+    if frames.dim() != 3 or frames.dtype != torch.uint8 or not frames.is_contiguous():
+        raise ValueError("frames must be a contiguous (F, H, W) uint8 tensor")
+    if not frames.is_cuda or not out.is_cuda or not offsets.is_cuda:
+        raise ValueError("detect_device needs CUDA (HIP) tensors")
+    if offsets.dtype != torch.int64 or offsets.numel() < frames.shape[0] + 1:
+        raise ValueError("offsets must be int64 with F+1 entries")
+    if out.dim() != 2 or out.shape[1] != 2 or out.element_size() != 4 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (cap, 2) 32-bit tensor")
+    dev = frames.device.index if device is None else device
+    cfg = _to_c_config(config)
+    ctx = context(dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(frames.device)
+    f, h, w = frames.shape
+    rc = _native.load().fdf_detect_device(
+        ctx.handle, frames.data_ptr(), f, w, h, h * w, ctypes.byref(cfg), out.data_ptr(),
+        out.shape[0], offsets.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+    check(rc, "fdf_detect_device")
+
+
+def keypoint_scores(img, points, config, device=0):
+    """u16 NMS scores of the given centres (extension: the reference's Point has no score).
+    ``config.non_maximal_supression`` picks MaxThreshold (src/fast_simd.rs:623-718, window =
+    count) or SumAbsolute (:722-749, uses threshold)."""
+    arr = _as_pixels(img)
+    pts = np.ascontiguousarray(np.asarray(points, dtype=np.uint32).reshape(-1, 2))
+    cfg = _to_c_config(config)
+    h, w = arr.shape
+    scores = np.zeros(pts.shape[0], dtype=np.uint16)
+    rc = _native.load().fdf_score_points(
+        context(device).handle, arr.ctypes.data, w, h, arr.strides[0], ctypes.byref(cfg),
+        pts.ctypes.data, pts.shape[0], scores.ctypes.data)
+    check(rc, "fdf_score_points")
+    return scores
+
+
+__all__ = ["NORTH", "EAST", "SOUTH", "WEST", "circle", "calculate_offsets", "context",
+           "detect_array", "detector", "detector_batch", "detect_device", "keypoint_scores",
+           "NonMaximalSuppression"]

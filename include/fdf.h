@@ -1,0 +1,137 @@
+/*
+ * fdf.h -- C ABI of the MI355X (gfx950) FAST-9..16 corner detector.
+ *
+ * Drop-in boundary for the reference's hot path `fast_simd::detector`
+ * (iwanders/feature_detector_fast src/fast_simd.rs:847-859), which the crate API calls from
+ * `Config::detect` (src/lib.rs:56-58) and `detect` (src/lib.rs:62-64).  Every entry point
+ * below names the reference interface it replaces.  A Rust shim that binds these symbols
+ * is shown in INTEGRATION.md; the C++ mirror of the crate API is include/fdf.hpp.
+ *
+ * Semantics are the reference's, bit for bit (SURVEY.md §7 "semantic contract"):
+ *   - centres x in [3, w-3), y in [3, h-3); circle order of src/fast_simd.rs:79-98;
+ *   - bright <=> p > c + t, dark <=> p < c - t (strict, integer);
+ *   - keypoint <=> a cyclic run of >= n bright or >= n dark circle pixels (9 <= n <= 16);
+ *   - NMS (MaxThreshold / SumAbsolute): keep iff y not in {3, h-4} and the score is strictly
+ *     greater than every 8-neighbour that is itself a keypoint (src/fast_simd.rs:589-616);
+ *   - output: points in raster order (y ascending, then x).
+ * Where the reference panics, these functions return an error code and never abort.
+ *
+ * Ownership: the caller owns every input and output buffer.  The library owns device
+ * workspace inside an opaque context, reused across calls.  No global mutable state.
+ * Threading: a context serialises its own host calls; distinct contexts may be used
+ * concurrently from different threads.  One context = one device + one HIP stream.
+ */
+#ifndef FDF_H
+#define FDF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDF_ABI_VERSION 1
+
+/* Status codes.  Shapes the reference maps to an empty Vec return FDF_OK with 0 points. */
+enum fdf_status {
+    FDF_OK = 0,
+    FDF_ERR_COUNT = 1,     /* count n outside [9, 16]: src/fast_simd.rs:302-305 (n<9), :800 (n>16) */
+    FDF_ERR_SIZE = 2,      /* h < 3, or h >= 7 with w < 6: the u32 underflows at :342 / :369 */
+    FDF_ERR_CAPACITY = 3,  /* output buffer too small; *n_out holds the required point count */
+    FDF_ERR_NMS = 4,       /* non_maximal_supression value not 0, 1 or 2 */
+    FDF_ERR_DEVICE = 5,    /* HIP runtime failure (no device, launch or copy error) */
+    FDF_ERR_ARG = 6,       /* NULL pointer, stride < width, or a size that overflows */
+    FDF_ERR_ALLOC = 7      /* device or pinned host allocation failed */
+};
+
+/* src/lib.rs:26-36 NonMaximalSuppression {Off, MaxThreshold, SumAbsolute}. */
+enum fdf_nms {
+    FDF_NMS_OFF = 0,
+    FDF_NMS_MAX_THRESHOLD = 1,
+    FDF_NMS_SUM_ABSOLUTE = 2
+};
+
+/* src/lib.rs:40-52 Config {threshold: u8, count: u8, non_maximal_supression}. */
+typedef struct fdf_config {
+    uint8_t threshold;
+    uint8_t count;
+    uint8_t nms; /* enum fdf_nms */
+} fdf_config;
+
+/* src/lib.rs:17-20 Point {x: u32, y: u32}, laid out as #[repr(C)]. */
+typedef struct fdf_point {
+    uint32_t x;
+    uint32_t y;
+} fdf_point;
+
+typedef struct fdf_ctx fdf_ctx;
+
+/* Library/ABI identification. */
+int fdf_abi_version(void);
+const char* fdf_status_string(int status);
+/* Number of visible HIP devices (0 when none); never fails. */
+int fdf_device_count(void);
+
+/* Validate a configuration and image shape without touching a device.  Returns FDF_OK and
+ * sets *empty = 1 for the shapes the reference answers with an empty Vec (3 <= h <= 6, or
+ * h >= 7 with w == 6); otherwise the error the reference would panic with. */
+int fdf_validate(uint32_t width, uint32_t height, const fdf_config* cfg, int* empty);
+
+/* Context: binds a device and creates a non-blocking HIP stream owned by the context. */
+int fdf_ctx_create(int device, fdf_ctx** out_ctx);
+void fdf_ctx_destroy(fdf_ctx* ctx);
+/* The context's hipStream_t (as void*), for callers that enqueue their own work beside it. */
+void* fdf_ctx_stream(fdf_ctx* ctx);
+
+/*
+ * Replaces fast_simd::detector(img, config) -> Vec<Point> (src/fast_simd.rs:847).
+ * Host image (row-major u8, `stride_bytes` >= width; GrayImage always has stride == width),
+ * host output.  Synchronous.  Two-call pattern: if `cap` is too small, returns
+ * FDF_ERR_CAPACITY with *n_out = the required count and writes the first `cap` points.
+ */
+int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+               size_t stride_bytes, const fdf_config* cfg, fdf_point* out, size_t cap,
+               size_t* n_out);
+
+/*
+ * Batched host variant: `n_frames` frames of width x height, frame f at
+ * data + f * frame_stride_bytes (rows packed, stride == width).  Output is every frame's
+ * list concatenated in frame order; frame f's points are out[frame_offsets[f] ..
+ * frame_offsets[f+1]) (frame_offsets has n_frames + 1 entries; may be NULL).
+ * Capacity semantics as fdf_detect.
+ */
+int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t width,
+                     uint32_t height, size_t frame_stride_bytes, const fdf_config* cfg,
+                     fdf_point* out, size_t cap, uint64_t* frame_offsets, size_t* n_out);
+
+/*
+ * Device-resident batched variant (the throughput path; nothing crosses PCIe).
+ * `d_frames`, `d_out` and `d_frame_offsets` are device pointers on the context's device.
+ * Asynchronous: enqueued on `stream` (a hipStream_t; NULL = the HIP null stream; pass
+ * fdf_ctx_stream(ctx) for the context's own stream).  On
+ * completion d_frame_offsets[0..n_frames] holds the exclusive prefix of per-frame counts
+ * and d_frame_offsets[n_frames] the total, even when the total exceeds `cap` (points with
+ * index >= cap are not written).  Argument and shape errors are returned synchronously.
+ * The context's workspace is reused by each call: calls on one context must be issued on
+ * one stream (or otherwise serialised).
+ */
+int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
+                      uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
+                      const fdf_config* cfg, fdf_point* d_out, uint64_t cap,
+                      uint64_t* d_frame_offsets, void* stream);
+
+/*
+ * Scores for given points (extension: the reference's Point carries no score; these are the
+ * u16 values its NMS compares, src/fast_simd.rs:623-718 and :722-749).  Host in/out,
+ * synchronous.  `nms` selects the score: MaxThreshold (window = cfg->count) or SumAbsolute
+ * (uses cfg->threshold).  Points must be centres (3 <= x < w-3, 3 <= y < h-3).
+ */
+int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+                     size_t stride_bytes, const fdf_config* cfg, const fdf_point* points,
+                     size_t n_points, uint16_t* out_scores);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FDF_H */

@@ -1,0 +1,33 @@
+/* fast_oracle.h -- TEST INFRASTRUCTURE ONLY: scalar CPU restatement of the reference's
+ * FAST semantics (see fast_oracle.c for the file:line it follows). */
+#ifndef FDF_FAST_ORACLE_H
+#define FDF_FAST_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Negative return codes of fdf_oracle_detect (mirror include/fdf.h's FDF_ERR_* values). */
+#define FDF_ORACLE_ERR_COUNT (-1)
+#define FDF_ORACLE_ERR_SIZE (-2)
+#define FDF_ORACLE_ERR_NMS (-4)
+#define FDF_ORACLE_ERR_ALLOC (-7)
+
+int fdf_oracle_is_corner(uint8_t center, const uint8_t circle[16], uint8_t t, uint8_t n);
+uint16_t fdf_oracle_score_max_threshold(uint8_t center, const uint8_t circle[16], uint8_t n);
+uint16_t fdf_oracle_score_sum_abs(uint8_t center, const uint8_t circle[16], uint8_t t);
+int fdf_oracle_check(uint32_t w, uint32_t h, uint8_t n, uint8_t nms, int* empty);
+
+/* Returns the keypoint count (>= 0; only the first `cap` are written as x,y pairs into
+ * out_xy and, if non-NULL, their NMS scores into out_scores) or a negative error code. */
+int64_t fdf_oracle_detect(const uint8_t* img, uint32_t w, uint32_t h, size_t stride,
+                          uint8_t t, uint8_t n, uint8_t nms, uint32_t* out_xy, size_t cap,
+                          uint16_t* out_scores);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,63 @@
+"""In-process A/B timing of detector variants (cdna_hip_programming.md §5.4 rule 24).
+
+Variants are selected through FDF_DEBUG_FLAGS (internal ablation switches of the band
+kernel, fdf_kernels.h) and the NMS mode; rounds are interleaved in one process on one
+device, and the median/min per variant are printed as JSON.
+    python tools/ablate.py [--frames 512] [--rounds 5] [--iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=512)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--variants", default="maxt:0,maxt:1,maxt:3,off:0,off:3,sad:0")
+    args = ap.parse_args()
+    import torch
+
+    import workloads
+    from feature_detector_fast_amd import Config, NonMaximalSuppression, fast_hip
+
+    frames = workloads.s1_frames_torch(0, args.frames, args.width, args.height)
+    out = torch.empty((args.frames * 50_000, 2), dtype=torch.int32, device="cuda")
+    offs = torch.zeros(args.frames + 1, dtype=torch.int64, device="cuda")
+    modes = {"off": 0, "maxt": 1, "sad": 2}
+    variants = [(v.split(":")[0], int(v.split(":")[1])) for v in args.variants.split(",")]
+    times = {v: [] for v in variants}
+    stream = torch.cuda.current_stream()
+    for r in range(args.rounds):
+        for (mode, flags) in variants:
+            os.environ["FDF_DEBUG_FLAGS"] = str(flags)
+            cfg = Config(16, 9, NonMaximalSuppression(modes[mode]))
+            fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(args.iters):
+                fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
+            e.record(stream)
+            torch.cuda.synchronize()
+            times[(mode, flags)].append(s.elapsed_time(e) / args.iters)
+    os.environ.pop("FDF_DEBUG_FLAGS", None)
+    px = args.frames * args.width * args.height
+    res = {}
+    for (mode, flags), ts in times.items():
+        med = float(np.median(ts))
+        res[f"{mode}:flags{flags}"] = {"ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+                                       "Gpix_s": round(px / med / 1e6, 1)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
