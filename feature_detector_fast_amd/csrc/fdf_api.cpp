@@ -21,11 +21,13 @@ struct fdf_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // device workspace, grown on demand
-    uint8_t* d_in = nullptr;            size_t in_bytes = 0;
-    uint2* d_out = nullptr;             size_t out_points = 0;
-    uint64_t* d_offsets = nullptr;      size_t offsets_n = 0;
-    unsigned long long* d_state = nullptr; size_t state_n = 0;
-    uint32_t* d_counter = nullptr;
+    uint8_t* d_in = nullptr;            size_t in_bytes = 0;       // host-API frame staging
+    uint2* d_out = nullptr;             size_t out_points = 0;     // host-API output
+    uint64_t* d_offsets = nullptr;      size_t offsets_n = 0;      // host-API frame offsets
+    uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
+    uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
+    unsigned long long* d_state = nullptr; size_t state_n = 0;     // compaction look-back
+    uint32_t* d_ticket = nullptr;
     uint32_t epoch = 0;
 };
 
@@ -75,32 +77,36 @@ int ensure(T** buf, size_t* have, size_t need, bool zero, hipStream_t stream) {
 
 // Band height: tall bands amortise the 8-row halo; short bands fill the 256 CUs when the
 // whole job is small (e.g. one frame).  Capped so the LDS layout fits.
-uint32_t pick_rows(uint32_t n_frames, uint32_t w, uint32_t h, bool nms) {
+uint32_t pick_rows(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score_bytes) {
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
     uint32_t R = 8;
     if ((uint64_t)n_frames * ((centre_rows + 7) / 8) < 1024) R = 4;
-    while (R > 1 && fdfk::make_layout(R, nw, nms).total > fdfk::kMaxLds) --R;
+    while (R > 1 && fdfk::make_layout(R, nw, score_bytes).total > fdfk::kMaxLds) --R;
     return R;
 }
 
-// Enqueue the band kernel over `n_frames` device frames.  Frames must be valid (w, h >= 7).
+// Enqueue detection + compaction over `n_frames` device frames (w, h >= 7).
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream) {
-    const bool nms = cfg->nms != FDF_NMS_OFF;
-    const uint32_t R = pick_rows(n_frames, w, h, nms);
+    const uint32_t sb = fdfk::score_bytes_for(cfg->nms);
+    const uint32_t R = pick_rows(n_frames, w, h, sb);
     const uint32_t nw = (w + 31) / 32;
-    if (fdfk::make_layout(R, nw, nms).total > fdfk::kMaxLds) return FDF_ERR_SIZE;
+    if (fdfk::make_layout(R, nw, sb).total > fdfk::kMaxLds) return FDF_ERR_SIZE;
     const uint32_t bands = (h - 6 + R - 1) / R;
     const uint64_t ntasks = (uint64_t)bands * n_frames;
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
-    int rc = ensure(&ctx->d_state, &ctx->state_n, (size_t)ntasks, true, stream);
-    if (rc) return rc;
-    if (!ctx->d_counter) {
-        if (hipMalloc(reinterpret_cast<void**>(&ctx->d_counter), sizeof(uint32_t)) != hipSuccess)
+    const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw);
+    const uint64_t ngroups = (ntasks + fdfk::kCompactTasks - 1) / fdfk::kCompactTasks;
+    int rc;
+    if ((rc = ensure(&ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), false, stream))) return rc;
+    if ((rc = ensure(&ctx->d_counts, &ctx->counts_n, (size_t)ntasks, false, stream))) return rc;
+    if ((rc = ensure(&ctx->d_state, &ctx->state_n, (size_t)ngroups, true, stream))) return rc;
+    if (!ctx->d_ticket) {
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->d_ticket), sizeof(uint32_t)) != hipSuccess)
             return FDF_ERR_ALLOC;
-        if (hipMemsetAsync(ctx->d_counter, 0, sizeof(uint32_t), stream) != hipSuccess)
+        if (hipMemsetAsync(ctx->d_ticket, 0, sizeof(uint32_t), stream) != hipSuccess)
             return FDF_ERR_DEVICE;
     }
     if (++ctx->epoch > 0xffffu) {   // generation tag wrapped: clear stale look-back words
@@ -109,6 +115,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
             hipSuccess)
             return FDF_ERR_DEVICE;
     }
+    const char* dbg = std::getenv("FDF_DEBUG_FLAGS");   // ablation runs only, see fdf_kernels.h
     fdfk::BandParams p;
     p.frames = d_frames;
     p.frame_stride = frame_stride;
@@ -119,15 +126,27 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.ntasks = (uint32_t)ntasks;
     p.words_per_row = nw;
     p.threshold = cfg->threshold;
-    p.epoch = ctx->epoch;
-    p.out = d_out;
-    p.cap = cap;
-    p.frame_offsets = d_offsets;
-    p.band_state = ctx->d_state;
-    p.task_counter = ctx->d_counter;
-    const char* dbg = std::getenv("FDF_DEBUG_FLAGS");   // ablation builds only, see fdf_kernels.h
+    p.slot_bytes = slot_bytes;
+    p.slots = ctx->d_slots;
+    p.counts = ctx->d_counts;
     p.flags = dbg ? (uint32_t)std::strtoul(dbg, nullptr, 0) : 0u;
-    if (fdfk::launch_band_kernel(p, cfg->nms, cfg->count, stream) != hipSuccess)
+    fdfk::CompactParams c;
+    c.width = w;
+    c.height = h;
+    c.rows = R;
+    c.bands_per_frame = bands;
+    c.ntasks = (uint32_t)ntasks;
+    c.words_per_row = nw;
+    c.slot_bytes = slot_bytes;
+    c.epoch = ctx->epoch;
+    c.slots = ctx->d_slots;
+    c.counts = ctx->d_counts;
+    c.out = d_out;
+    c.cap = cap;
+    c.frame_offsets = d_offsets;
+    c.state = ctx->d_state;
+    c.ticket = ctx->d_ticket;
+    if (fdfk::launch_detect(p, c, cfg->nms, cfg->count, stream) != hipSuccess)
         return FDF_ERR_DEVICE;
     return FDF_OK;
 }
@@ -248,8 +267,10 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_in);
         (void)hipFree(ctx->d_out);
         (void)hipFree(ctx->d_offsets);
+        (void)hipFree(ctx->d_slots);
+        (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_state);
-        (void)hipFree(ctx->d_counter);
+        (void)hipFree(ctx->d_ticket);
         (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;

@@ -1,32 +1,34 @@
 // fdf_kernels.hip -- FAST-9..16 corner detection for MI355X (gfx950, CDNA4).
 //
-// One fused kernel replaces the reference's hot path below the host/device boundary:
-// detect<NONMAX>() (iwanders/feature_detector_fast src/fast_simd.rs:301-620) together with
-// determine_keypoint (:115-297) and the two NMS score functions (:623-718, :722-749).
+// Two kernels replace the reference's hot path below the host/device boundary:
+// detect<NONMAX>() (iwanders/feature_detector_fast src/fast_simd.rs:301-620) with
+// determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
 //
-// Work decomposition:
-//   * task  = one band of R full-width centre rows of one frame; tasks are numbered in
-//             output (raster, frame-major) order and handed out by a device-wide atomic
-//             counter, so a task's predecessors are always resident or finished.
-//   * chunk = the band is swept left to right in 1024-column chunks.  Each chunk's input
-//             (R+8 rows x 1056 bytes, 16-B aligned) is staged into LDS with 16-B loads.
-//   * pre-filter: each lane takes a 4-pixel group (one LDS dword), unpacks it into two
-//             packed-u16 pairs and runs the cardinal test with v_pk_{max,min,sub}_u16.
-//             Exact reformulation of src/fast_simd.rs:441-509: 2-of-4 adjacent cardinals
-//             <=> min(max(N,S), max(E,W)) > c+t (dark: max(min(N,S), min(E,W)) < c-t);
-//             3-of-4 <=> 2nd smallest > c+t (dark: 2nd largest < c-t).
-//   * candidate queue: lanes whose group has a candidate append it to a per-wave LDS
-//             queue; every 16 queued groups are tested densely (4 lanes per group).
-//   * full test: the 16 circle bytes come from LDS with immediate offsets; the
-//             bright/dark classifications become 32 wave ballots (bit-sliced masks over
-//             64 candidates) and the cyclic run test runs on them as scalar 64-bit ANDs.
-//   * NMS: scores go to an LDS score map (R+2 rows incl. the 1-pixel ring); keypoints of
-//             the band's own rows go to an LDS list; the 3x3 strict-max test runs over that
-//             list.  Keep-bits are set in an LDS band bitmap.
-//   * ordered output: decoupled look-back across tasks yields each band's global offset;
-//             the bitmap is expanded into (x, y) points already in raster order.
+// fast_band_kernel -- one workgroup per band of R full-width centre rows of one frame
+// (DESIGN.md §3).  The band is swept in 1024-column chunks staged into LDS; per chunk:
+//   * pre-filter: a lane takes a 4-pixel group (one LDS dword) and runs the cardinal test
+//     on all 4 bytes at once.  v_lerp_u8 gives exact per-byte comparisons: with
+//     v = lerp(X, ~c, r) = (X - c + 255 + r) >> 1, "X - c > t" is bit 7 of lerp(v, Kb, 0)
+//     for r = t & 1, Kb = 128 - ceil(t/2); "X - c < -t" is the complement of bit 7 of
+//     lerp(lerp(X, ~c, 1 - (t & 1)), Kd, 0), Kd = 255 - ((254 - t + (1 - (t & 1))) >> 1).
+//     2-of-4 adjacent cardinals (src/fast_simd.rs:441-472) and 3-of-4 (:473-506) are then
+//     bitwise logic on the flags.  The pre-filter is only a necessary condition.
+//   * candidate queues: groups with candidates go to a per-wave LDS queue; 16 groups at a
+//     time are expanded into a per-wave queue of candidate pixels.
+//   * full test, 64 candidate pixels per wave: the 16 circle bytes come from LDS with
+//     immediate offsets; the 32 bright/dark classifications are wave ballots (bit-sliced
+//     masks over the 64 lanes) and the cyclic run test is scalar 64-bit AND/OR.
+//   * NMS: scores go to an LDS score map with a 1-pixel ring (u8 for max-threshold, whose
+//     score is <= 255; u16 for SAD); keypoints of the chunk's own pixels go to a list and
+//     the 3x3 strict-max test (:589-616) runs over that list into an LDS band bitmap.
+//   * output: the band's points in raster order go to its fixed-size slot (or, if they do
+//     not fit, its bitmap) with the count in counts[task]; no inter-workgroup waiting.
+// compact_kernel -- scans the band counts in raster order (decoupled look-back over
+//   workgroups of 256 bands) and copies each band's slot to its final position.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "fdf_kernels.h"
 
@@ -44,64 +46,67 @@ __host__ __device__ constexpr int circle_dy(int i) {
     return dy[i];
 }
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kHigh = 0x80808080u;
 
-__device__ __forceinline__ u16x2 as_pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ u16x2 pk_max(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
-__device__ __forceinline__ u16x2 pk_min(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
-__device__ __forceinline__ u16x2 pk_subs(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
-
-// v_perm_b32: bytes 0-3 of the 8-byte source {hi, lo} come from `lo`, 4-7 from `hi`;
-// selector byte 0x0c produces 0x00.
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-    return __builtin_amdgcn_perm(hi, lo, sel);
+__device__ __forceinline__ uint32_t lerp_u8(uint32_t a, uint32_t b, uint32_t r) {
+    return __builtin_amdgcn_lerp(a, b, r);
+}
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+// v_cmp straight into an SGPR pair (HIP's __ballot(int) round-trips the bool through a VGPR).
+__device__ __forceinline__ uint64_t wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Cardinal pre-filter for one pair of centres held as packed u16 (c, north, south, east,
-// west); returns a u32 whose u16 halves are non-zero iff that centre is a candidate.
+// Per-launch byte constants of the lerp comparisons (threshold t < 255).
+struct LerpConsts {
+    uint32_t rb, kb, rd, kd;
+};
+__device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
+    LerpConsts k;
+    const uint32_t ob = t & 1u, od = (t + 1u) & 1u;
+    k.rb = ob * 0x01010101u;
+    k.kb = (128u - ((t + ob) >> 1)) * 0x01010101u;
+    k.rd = od * 0x01010101u;
+    k.kd = (255u - ((254u - t + od) >> 1)) * 0x01010101u;
+    return k;
+}
+
+// Cardinal pre-filter of the 4 centres at `px` (tile address of the group's first byte).
+// Returns bit 7 of byte j set iff centre j passes (a necessary condition for a keypoint).
 template <int N>
-__device__ __forceinline__ uint32_t prefilter_pair(u16x2 c, u16x2 nn, u16x2 ss, u16x2 ee,
-                                                   u16x2 ww, u16x2 t2) {
-    const u16x2 upper = c + t2;             // no overflow in u16: c, t <= 255
-    const u16x2 lower = pk_subs(c, t2);     // saturating: c - t clamped at 0
-    const u16x2 a = pk_max(nn, ss), cmn = pk_min(nn, ss);
-    const u16x2 b = pk_max(ee, ww), dmn = pk_min(ee, ww);
-    u16x2 bv, dv;
+__device__ __forceinline__ uint32_t prefilter_group(const uint8_t* px, const LerpConsts& k) {
+    const uint32_t c = *reinterpret_cast<const uint32_t*>(px);
+    const uint32_t l = *reinterpret_cast<const uint32_t*>(px - 4);
+    const uint32_t r = *reinterpret_cast<const uint32_t*>(px + 4);
+    const uint32_t n = *reinterpret_cast<const uint32_t*>(px - 3 * kPitch);
+    const uint32_t s = *reinterpret_cast<const uint32_t*>(px + 3 * kPitch);
+    const uint32_t nc = ~c;
+    const uint32_t e = alignbyte(r, c, 3);   // x+3 .. x+6
+    const uint32_t w = alignbyte(c, l, 1);   // x-3 .. x
+    // bright: bit 7 <=> X - c > t ; ndark: bit 7 <=> NOT(X - c < -t)
+    const uint32_t bn = lerp_u8(lerp_u8(n, nc, k.rb), k.kb, 0);
+    const uint32_t be = lerp_u8(lerp_u8(e, nc, k.rb), k.kb, 0);
+    const uint32_t bs = lerp_u8(lerp_u8(s, nc, k.rb), k.kb, 0);
+    const uint32_t bw = lerp_u8(lerp_u8(w, nc, k.rb), k.kb, 0);
+    const uint32_t dn = lerp_u8(lerp_u8(n, nc, k.rd), k.kd, 0);
+    const uint32_t de = lerp_u8(lerp_u8(e, nc, k.rd), k.kd, 0);
+    const uint32_t ds = lerp_u8(lerp_u8(s, nc, k.rd), k.kd, 0);
+    const uint32_t dw = lerp_u8(lerp_u8(w, nc, k.rd), k.kd, 0);
+    uint32_t bright, not_dark;
     if constexpr (N < 12) {
-        bv = pk_min(a, b);       // bright on 2 adjacent cardinals
-        dv = pk_max(cmn, dmn);   // dark on 2 adjacent cardinals
+        // 2 adjacent of 4 <=> (N|S) & (E|W)  (every N/S-E/W pair is adjacent)
+        bright = (bn | bs) & (be | bw);
+        not_dark = (dn & ds) | (de & dw);                       // NOT((dN|dS) & (dE|dW))
     } else {
-        const u16x2 p = pk_max(cmn, dmn), q = pk_min(a, b);
-        bv = pk_min(p, q);       // 2nd smallest of the four cardinals
-        dv = pk_max(p, q);       // 2nd largest
+        // 3 of 4 (any three cardinals are consecutive)
+        bright = (bn & bs & (be | bw)) | (be & bw & (bn | bs));
+        not_dark = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));   // >= 2 not dark
     }
-    return as_u32(pk_subs(bv, upper)) | as_u32(pk_subs(lower, dv));
-}
-
-// Bytes 0..3 of the result are non-zero iff centre j of the group is a candidate.
-template <int N>
-__device__ __forceinline__ uint32_t prefilter_group(const uint8_t* tile_px, uint32_t t) {
-    const uint32_t c = *reinterpret_cast<const uint32_t*>(tile_px);
-    const uint32_t l = *reinterpret_cast<const uint32_t*>(tile_px - 4);
-    const uint32_t r = *reinterpret_cast<const uint32_t*>(tile_px + 4);
-    const uint32_t n = *reinterpret_cast<const uint32_t*>(tile_px - 3 * kPitch);
-    const uint32_t s = *reinterpret_cast<const uint32_t*>(tile_px + 3 * kPitch);
-    const u16x2 t2 = {(unsigned short)t, (unsigned short)t};
-    // even centres (bytes 0, 2) and odd centres (bytes 1, 3) of the group
-    const uint32_t even = prefilter_pair<N>(
-        as_pk(perm(0, c, 0x0c020c00)), as_pk(perm(0, n, 0x0c020c00)),
-        as_pk(perm(0, s, 0x0c020c00)),
-        as_pk(perm(r, c, 0x0c050c03)),   // east:  x+3, x+5
-        as_pk(perm(c, l, 0x0c030c01)),   // west:  x-3, x-1
-        t2);
-    const uint32_t odd = prefilter_pair<N>(
-        as_pk(perm(0, c, 0x0c030c01)), as_pk(perm(0, n, 0x0c030c01)),
-        as_pk(perm(0, s, 0x0c030c01)),
-        as_pk(perm(r, c, 0x0c060c04)),   // east:  x+4, x+6
-        as_pk(perm(c, l, 0x0c040c02)),   // west:  x-2, x
-        t2);
-    return even | (odd << 8);            // halves <= 255, so bytes = centres 0..3
+    return (bright | ~not_dark) & kHigh;
 }
 
 // Cyclic run test on bit-sliced masks: bit k of b[i] = "lane k's circle pixel i qualifies".
@@ -159,117 +164,134 @@ __device__ __forceinline__ uint32_t score_sum_abs(uint32_t c, const uint32_t (&p
     return max(sb, sd);
 }
 
-__device__ __forceinline__ uint32_t lane_id() {
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
+template <typename ScoreT>
 struct Smem {
-    uint8_t* tile;       // (R+8) x kPitch input bytes
-    uint16_t* scores;    // (R+2) x kScorePitch u16 scores (NMS only)
+    uint8_t* tile;       // (R+8) x kPitch input bytes; tile (r, c) = image (y0-4+r, X0-16+c)
+    ScoreT* scores;      // (R+2) x kScorePitch; score (s, col) = image (y0-1+s, X0-4+col)
     uint32_t* bitmap;    // R x words_per_row keep-bits of the band
-    uint32_t* q_item;    // kWaves x kQueueCap queued groups: (s << 12) | gi
-    uint32_t* q_cand;    // kWaves x kQueueCap candidate bytes of the queued group
-    uint32_t* kp_list;   // kKpCap keypoints of the band's own rows: (s << 16) | score col
-    uint32_t* misc;      // [0] keypoint-list length, [1] look-back result lo/hi, wave sums
+    uint32_t* gq_item;   // kWaves x kGroupQ queued groups: (s << 12) | gi
+    uint32_t* gq_cand;   // kWaves x kGroupQ candidate flags (bit 7 of byte j = pixel j)
+    uint32_t* pq;        // kWaves x kPixelQ queued pixels: (s << 12) | col
+    uint32_t* kp_list;   // kKpCap keypoints of the chunk's own pixels: (s << 16) | col
+    uint32_t* misc;      // [0] keypoint-list length, [4..] per-wave sums
 };
 
-__device__ __forceinline__ Smem carve(uint8_t* base, const LdsLayout& L) {
-    Smem s;
+template <typename ScoreT>
+__device__ __forceinline__ Smem<ScoreT> carve(uint8_t* base, const LdsLayout& L) {
+    Smem<ScoreT> s;
     s.tile = base + L.tile;
-    s.scores = reinterpret_cast<uint16_t*>(base + L.scores);
+    s.scores = reinterpret_cast<ScoreT*>(base + L.scores);
     s.bitmap = reinterpret_cast<uint32_t*>(base + L.bitmap);
-    s.q_item = reinterpret_cast<uint32_t*>(base + L.q_item);
-    s.q_cand = reinterpret_cast<uint32_t*>(base + L.q_cand);
+    s.gq_item = reinterpret_cast<uint32_t*>(base + L.gq_item);
+    s.gq_cand = reinterpret_cast<uint32_t*>(base + L.gq_cand);
+    s.pq = reinterpret_cast<uint32_t*>(base + L.pq);
     s.kp_list = reinterpret_cast<uint32_t*>(base + L.kp_list);
     s.misc = reinterpret_cast<uint32_t*>(base + L.misc);
     return s;
 }
 
-// Dense test of up to 16 queued groups, 4 lanes per group (lane = 4*entry + pixel).
-template <int NMS, int N>
-__device__ __forceinline__ void test_queued(const Smem& sm, const uint32_t* qi,
-                                            const uint32_t* qc, uint32_t count, uint32_t t,
-                                            uint32_t X0, uint32_t rows, uint32_t nw) {
-    const uint32_t lane = lane_id();
-    const uint32_t e = lane >> 2, j = lane & 3;
-    bool act = e < count;
-    const uint32_t item = act ? qi[e] : 0u;
-    const uint32_t cand = act ? qc[e] : 0u;
-    act = act && ((cand >> (8 * j)) & 0xffu) != 0;
-    const uint32_t s = item >> 12, gi = item & 0xfffu;
-    // top-left of the 7x7 neighbourhood: tile row (s+3)-3, tile column (12+4gi+j)-3
-    const uint8_t* nb = sm.tile + s * kPitch + 9 + 4 * gi + j;
+struct ChunkCtx {
+    uint32_t t;        // threshold
+    uint32_t X0;       // first image column of the chunk
+    uint32_t rows;     // centre rows of the band
+    uint32_t nw;       // bitmap words per row
+};
+
+// Full test of `count` (<= 64) queued pixels, one per lane, starting at pq[0].
+template <int NMS, int N, typename ScoreT>
+__device__ __forceinline__ void test_pixels(const Smem<ScoreT>& sm, const uint32_t* pq,
+                                            uint32_t count, const ChunkCtx& cc, uint32_t lane) {
+    const bool act = lane < count;
+    const uint32_t code = act ? pq[lane] : 0u;
+    const uint32_t s = code >> 12, col = code & 0xfffu;
+    // top-left of the 7x7 neighbourhood: tile row (s+3)-3, tile column (12+col)-3
+    const uint8_t* nb = sm.tile + s * kPitch + 9 + col;
     const uint32_t c = nb[3 * kPitch + 3];
     uint32_t p[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) p[i] = nb[(circle_dy(i) + 3) * kPitch + circle_dx(i) + 3];
-    const int upper = (int)(c + t), lower = (int)c - (int)t;
+    const int upper = (int)(c + cc.t), lower = (int)c - (int)cc.t;
+    const uint64_t active = wave_ballot(act);
     uint64_t bright[16], dark[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bright[i] = __ballot(act && (int)p[i] > upper);
+    for (int i = 0; i < 16; ++i) bright[i] = wave_ballot((int)p[i] > upper) & active;
     const uint64_t kb = arc_test<N>(bright);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dark[i] = __ballot(act && (int)p[i] < lower);
+    for (int i = 0; i < 16; ++i) dark[i] = wave_ballot((int)p[i] < lower) & active;
     const uint64_t kd = arc_test<N>(dark);
-    const bool is_kp = ((kb | kd) >> lane) & 1u;
-    if (!is_kp) return;
-    const uint32_t col = 4 * gi + j;                   // score-map column
+    if (!(((kb | kd) >> lane) & 1u)) return;
     if constexpr (NMS == kNmsOff) {
-        const uint32_t x = X0 - 4 + col;
-        atomicOr(&sm.bitmap[(s - 1) * nw + (x >> 5)], 1u << (x & 31));
+        const uint32_t x = cc.X0 - 4 + col;
+        atomicOr(&sm.bitmap[(s - 1) * cc.nw + (x >> 5)], 1u << (x & 31));
     } else {
         const uint32_t score = NMS == kNmsMaxThreshold
                                    ? score_max_threshold<N>(c, p, ((kd >> lane) & 1u) != 0)
-                                   : score_sum_abs(c, p, t);
-        sm.scores[s * kScorePitch + col] = (uint16_t)score;
+                                   : score_sum_abs(c, p, cc.t);
+        sm.scores[s * kScorePitch + col] = (ScoreT)score;
         // the band's own rows and the chunk's own columns go to the NMS list
-        if (s >= 1 && s <= rows && col >= 4 && col < 4 + kChunk) {
+        if (s >= 1 && s <= cc.rows && col >= 4 && col < 4 + kChunk) {
             const uint32_t k = atomicAdd(&sm.misc[0], 1u);
             if (k < kKpCap) sm.kp_list[k] = (s << 16) | col;
         }
     }
 }
 
-__device__ __forceinline__ bool nms_keep(const uint16_t* sc) {
+// Expand `ng` (<= 16) queued groups into the pixel queue; returns the new pixel count.
+__device__ __forceinline__ uint32_t expand_groups(const uint32_t* gi_q, const uint32_t* gc_q,
+                                                  uint32_t ng, uint32_t* pq, uint32_t pcount,
+                                                  uint32_t lane) {
+    const bool act = lane < ng;
+    const uint32_t item = act ? gi_q[lane] : 0u;
+    const uint32_t cand = act ? gc_q[lane] : 0u;
+    const uint32_t cnt = __popc(cand);
+    const uint64_t b0 = wave_ballot(cnt > 0), b1 = wave_ballot(cnt > 1);
+    const uint64_t b2 = wave_ballot(cnt > 2), b3 = wave_ballot(cnt > 3);
+    uint32_t pos = pcount + lanes_below(b0) + lanes_below(b1) + lanes_below(b2) +
+                   lanes_below(b3);
+    const uint32_t code = ((item >> 12) << 12) | (4 * (item & 0xfffu));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (cand & (0x80u << (8 * j))) pq[pos++] = code + j;
+    }
+    return pcount + (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+}
+
+template <typename ScoreT>
+__device__ __forceinline__ bool nms_keep(const ScoreT* sc) {
     const uint32_t v = sc[0];
     constexpr int P = kScorePitch;
     return v > sc[-P - 1] && v > sc[-P] && v > sc[-P + 1] && v > sc[-1] && v > sc[1] &&
            v > sc[P - 1] && v > sc[P] && v > sc[P + 1];
 }
 
-__device__ __forceinline__ unsigned long long lb_pack(uint32_t epoch, uint32_t flag,
-                                                      unsigned long long value) {
-    return ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | value;
-}
-
 template <int NMS, int N>
 __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
+    using ScoreT = typename std::conditional<NMS == kNmsSumAbsolute, uint16_t, uint8_t>::type;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    const LdsLayout L = make_layout(P.rows, P.words_per_row, NMS != kNmsOff);
-    const Smem sm = carve(smem_raw, L);
+    const LdsLayout L = make_layout(P.rows, P.words_per_row, score_bytes_for(NMS));
+    const Smem<ScoreT> sm = carve<ScoreT>(smem_raw, L);
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = tid >> 6;
     const uint32_t lane = tid & 63;
     const uint32_t W = P.width, H = P.height, nw = P.words_per_row, t = P.threshold;
 
-    // ---- task id in dispatch order (decoupled look-back needs resident predecessors)
-    if (tid == 0) {
-        const uint32_t task = atomicAdd(P.task_counter, 1u);
-        if (task == P.ntasks - 1) atomicExch(P.task_counter, 0u);   // last ticket: reset
-        sm.misc[2] = task;
-    }
-    __syncthreads();
-    const uint32_t task = sm.misc[2];
+    // ---- task: XCD-aware static mapping.  Blocks b and b+8 share an XCD (round-robin
+    //      dispatch), so XCD k gets a contiguous run of bands and their shared halo rows
+    //      stay in its L2.  Bijective for any ntasks.
+    const uint32_t b = blockIdx.x;
+    const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
+    const uint32_t task = k8 * q8 + min(k8, r8) + (b >> 3);
     const uint32_t frame = task / P.bands_per_frame;
     const uint32_t band = task - frame * P.bands_per_frame;
-    const uint32_t y0 = 3 + band * P.rows;                         // first centre row
+    const uint32_t y0 = 3 + band * P.rows;                          // first centre row
     const uint32_t rows = min(P.rows, H - 3 - y0);                  // centre rows in band
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
 
+    if (t >= 255) {                                                  // no pixel can pass
+        if (tid == 0) P.counts[task] = 0;
+        return;
+    }
+    const LerpConsts lk = lerp_consts(t);
     for (uint32_t i = tid; i < rows * nw; i += kThreads) sm.bitmap[i] = 0;
 
     // score rows s <-> image row y0 - 1 + s; the 1-row ring exists only for NMS
@@ -277,6 +299,7 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
     const uint32_t s_hi = NMS == kNmsOff ? rows + 1 : rows + 2;
     const uint32_t tr_lo = NMS == kNmsOff ? 1 : 0;                  // tile rows to load
     const uint32_t tr_hi = NMS == kNmsOff ? rows + 7 : rows + 8;
+    const bool aligned_rows = (W & 15) == 0 && ((uintptr_t)img & 15) == 0;
 
     for (uint32_t X0 = 0; X0 < W - 3; X0 += kChunk) {
         __syncthreads();   // previous chunk's readers are done with the tile
@@ -291,16 +314,16 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
             uint4 val = make_uint4(0, 0, 0, 0);
             if (y >= 0 && y < (int)H && xc < (int)W && xc + 16 > 0) {
                 const uint8_t* src = img + (uint64_t)y * W + xc;
-                if (xc >= 0 && xc + 16 <= (int)W && ((uintptr_t)src & 15) == 0) {
+                if (aligned_rows && xc >= 0 && xc + 16 <= (int)W) {
                     val = *reinterpret_cast<const uint4*>(src);
                 } else {
-                    uint8_t b[16];
+                    uint8_t bb[16];
 #pragma unroll
                     for (int k = 0; k < 16; ++k) {
                         const int x = xc + k;
-                        b[k] = (x >= 0 && x < (int)W) ? src[k] : 0;
+                        bb[k] = (x >= 0 && x < (int)W) ? src[k] : 0;
                     }
-                    val = *reinterpret_cast<uint4*>(b);
+                    val = *reinterpret_cast<uint4*>(bb);
                 }
             }
             *reinterpret_cast<uint4*>(sm.tile + tr * kPitch + tv * 16) = val;
@@ -308,10 +331,10 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         if (NMS != kNmsOff && tid == 0) sm.misc[0] = 0;
         __syncthreads();
 
-        // ---- groups gi <-> image columns X0-4+4gi .. +3; only those touching the needed
-        //      columns: centres [X0, X0+kChunk) within [3, W-3), plus for NMS the ring
-        //      columns X0-1 and X0+kChunk, clamped to [2, W-3] (ring cells outside the
-        //      centre domain are processed so that their score is written as 0)
+        // ---- groups gi <-> image columns X0-4+4gi .. +3, limited to those touching the
+        //      needed columns: centres [X0, X0+kChunk) within [3, W-3), plus for NMS the
+        //      ring columns X0-1 and X0+kChunk clamped to [2, W-3] (ring cells outside the
+        //      centre domain are processed so their score is written as 0)
         const int need_lo = NMS == kNmsOff ? max((int)X0, 3) : max((int)X0 - 1, 2);
         const int need_hi = NMS == kNmsOff ? min((int)X0 + kChunk - 1, (int)W - 4)
                                            : min((int)X0 + kChunk, (int)W - 3);
@@ -319,10 +342,13 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         const uint32_t g_hi = ((uint32_t)(need_hi - ((int)X0 - 4)) >> 2) + 1;
         const uint32_t ng = g_hi - g_lo;
         const uint32_t nitems = (s_hi - s_lo) * ng;
+        const ChunkCtx cc{t, X0, rows, nw};
 
-        uint32_t* qi = sm.q_item + wave * kQueueCap;
-        uint32_t* qc = sm.q_cand + wave * kQueueCap;
-        uint32_t qcount = 0;
+        uint32_t* gqi = sm.gq_item + wave * kGroupQ;
+        uint32_t* gqc = sm.gq_cand + wave * kGroupQ;
+        uint32_t* pq = sm.pq + wave * kPixelQ;
+        uint32_t gcount = 0, pcount = 0;
+        const bool no_test = (P.flags & kFlagNoFullTest) != 0;
         // this lane's first item, then advance by kThreads items per round
         uint32_t item = wave * 64 + lane;
         uint32_t s = s_lo + item / ng;
@@ -330,8 +356,7 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         for (uint32_t base = wave * 64; base < nitems; base += kThreads) {
             uint32_t cand = 0;
             if (item < nitems) {
-                const uint8_t* px = sm.tile + (s + 3) * kPitch + 12 + 4 * gi;
-                cand = prefilter_group<N>(px, t);
+                cand = prefilter_group<N>(sm.tile + (s + 3) * kPitch + 12 + 4 * gi, lk);
                 const int y = (int)y0 - 1 + (int)s;
                 const int x0 = (int)X0 - 4 + 4 * (int)gi;
                 if (y < 3 || y >= (int)H - 3) cand = 0;
@@ -339,31 +364,41 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
                     uint32_t vm = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (x0 + j >= 3 && x0 + j < (int)W - 3) vm |= 0xffu << (8 * j);
+                        if (x0 + j >= 3 && x0 + j < (int)W - 3) vm |= 0x80u << (8 * j);
                     cand &= vm;
                 }
                 if constexpr (NMS != kNmsOff) {
-                    *reinterpret_cast<uint2*>(sm.scores + s * kScorePitch + 4 * gi) =
-                        make_uint2(0, 0);
+                    ScoreT* sp = sm.scores + s * kScorePitch + 4 * gi;
+                    if constexpr (sizeof(ScoreT) == 1) *reinterpret_cast<uint32_t*>(sp) = 0;
+                    else *reinterpret_cast<uint2*>(sp) = make_uint2(0, 0);
                 }
             }
-            const bool has = cand != 0;
-            const uint64_t bal = __ballot(has);
+            const bool has = cand != 0 && !no_test;
+            const uint64_t bal = wave_ballot(has);
             if (has) {
-                const uint32_t pos = qcount + lanes_below(bal);
-                qi[pos] = (s << 12) | gi;
-                qc[pos] = cand;
+                const uint32_t pos = gcount + lanes_below(bal);
+                gqi[pos] = (s << 12) | gi;
+                gqc[pos] = cand;
             }
-            qcount += (uint32_t)__popcll(bal);
-            while (qcount >= 16) {
-                qcount -= 16;
-                test_queued<NMS, N>(sm, qi + qcount, qc + qcount, 16, t, X0, rows, nw);
+            gcount += (uint32_t)__popcll(bal);
+            while (gcount >= 16) {
+                gcount -= 16;
+                pcount = expand_groups(gqi + gcount, gqc + gcount, 16, pq, pcount, lane);
+                while (pcount >= 64) {
+                    pcount -= 64;
+                    test_pixels<NMS, N>(sm, pq + pcount, 64, cc, lane);
+                }
             }
             item += kThreads;
             gi += kThreads;
             while (gi >= g_hi) { gi -= ng; ++s; }
         }
-        if (qcount > 0) test_queued<NMS, N>(sm, qi, qc, qcount, t, X0, rows, nw);
+        if (gcount > 0) pcount = expand_groups(gqi, gqc, gcount, pq, pcount, lane);
+        while (pcount > 0) {
+            const uint32_t take = min(pcount, 64u);
+            pcount -= take;
+            test_pixels<NMS, N>(sm, pq + pcount, take, cc, lane);
+        }
 
         if constexpr (NMS != kNmsOff) {
             __syncthreads();
@@ -386,7 +421,7 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
                     const uint32_t ss = 1 + k / kChunk, col = 4 + k % kChunk;
                     const uint32_t x = X0 - 4 + col, y = y0 - 1 + ss;
                     if (x < 3 || x >= W - 3 || y == 3 || y == H - 4) continue;
-                    const uint16_t* sc = sm.scores + ss * kScorePitch + col;
+                    const ScoreT* sc = sm.scores + ss * kScorePitch + col;
                     if (sc[0] != 0 && nms_keep(sc))
                         atomicOr(&sm.bitmap[(ss - 1) * nw + (x >> 5)], 1u << (x & 31));
                 }
@@ -401,7 +436,6 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
     const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);
     uint32_t mine = 0;
     for (uint32_t w = w_lo; w < w_hi; ++w) mine += __popc(sm.bitmap[w]);
-    // block exclusive scan of `mine`
     uint32_t incl = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -418,78 +452,165 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         before += (uint32_t)w < wave ? v : 0u;
         total += v;
     }
-    const uint32_t excl_in_band = before + incl - mine;
+    if (tid == 0) P.counts[task] = total;
+    if (P.flags & kFlagNoEmit) return;
 
-    // ---- decoupled look-back over tasks (raster order): band's global offset.  Wave 0
-    //      probes 64 predecessors per round (lane k reads task - 1 - k): the nearest
-    //      inclusive prefix ends the walk; a window of aggregates is summed and skipped.
-    if (wave == 0 && !(P.flags & kFlagNoLookback)) {
-        unsigned long long* st = P.band_state;
+    // ---- band slot: points in raster order when they fit, else the keep-bitmap
+    uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
+    if (total <= P.slot_bytes / 8) {
+        uint2* pts = reinterpret_cast<uint2*>(slot);
+        uint32_t idx = before + incl - mine;
+        for (uint32_t w = w_lo; w < w_hi; ++w) {
+            uint32_t bits = sm.bitmap[w];
+            const uint32_t r = w / nw;
+            const uint32_t xb = (w - r * nw) * 32;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                pts[idx++] = make_uint2(xb + bit, y0 + r);
+            }
+        }
+    } else {
+        uint32_t* words = reinterpret_cast<uint32_t*>(slot);
+        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = sm.bitmap[w];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Compaction: raster-order prefix over band counts, then slot -> final position copy.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long lb_pack(uint32_t epoch, uint32_t flag,
+                                                      unsigned long long value) {
+    return ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | value;
+}
+
+__global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P) {
+    __shared__ uint32_t s_task_off[kCompactTasks];
+    __shared__ uint32_t s_wave_sum[kCompactTasks / 64];
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_group;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t ngroups = (P.ntasks + kCompactTasks - 1) / kCompactTasks;
+    if (tid == 0) {   // groups in dispatch order: a group's predecessors are resident or done
+        const uint32_t g = atomicAdd(P.ticket, 1u);
+        if (g == ngroups - 1) atomicExch(P.ticket, 0u);
+        s_group = g;
+    }
+    __syncthreads();
+    const uint32_t g = s_group;
+    const uint32_t task = g * kCompactTasks + tid;
+    const uint32_t cnt = task < P.ntasks ? P.counts[task] : 0u;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += o;
+    }
+    if (lane == 63) s_wave_sum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kCompactTasks / 64; ++w) {
+        const uint32_t v = s_wave_sum[w];
+        before += (uint32_t)w < wave ? v : 0u;
+        total += v;
+    }
+    s_task_off[tid] = before + incl - cnt;
+
+    // decoupled look-back: wave 0 probes 64 predecessor groups per round
+    if (wave == 0) {
         unsigned long long excl = 0;
-        if (task == 0) {
+        if (g == 0) {
             if (lane == 0)
-                __hip_atomic_store(&st[0], lb_pack(P.epoch, 2, total), __ATOMIC_RELAXED,
+                __hip_atomic_store(&P.state[0], lb_pack(P.epoch, 2, total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (lane == 0)
-                __hip_atomic_store(&st[task], lb_pack(P.epoch, 1, total), __ATOMIC_RELAXED,
+                __hip_atomic_store(&P.state[g], lb_pack(P.epoch, 1, total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            int64_t top = (int64_t)task - 1;
+            int64_t top = (int64_t)g - 1;
             while (true) {
                 const int64_t idx = top - (int64_t)lane;
-                uint32_t flag = 2;                                   // before task 0: 0 incl.
+                uint32_t flag = 2;                                   // before group 0: 0 incl.
                 unsigned long long val = 0;
                 if (idx >= 0) {
                     const unsigned long long wv = __hip_atomic_load(
-                        &st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        &P.state[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     flag = (uint32_t)(wv >> 48) == P.epoch ? (uint32_t)(wv >> 46) & 3u : 0u;
                     val = wv & ((1ull << 46) - 1);
                 }
-                const uint64_t incl = __ballot(flag == 2);
-                const uint64_t missing = __ballot(flag == 0);
-                // lanes that matter: up to and including the nearest inclusive, else all 64
-                const uint64_t upto = incl ? (incl & (~incl + 1)) * 2 - 1 : ~0ull;
-                if (missing & upto) {                                // a predecessor not yet
-                    __builtin_amdgcn_s_sleep(2);                     // published: re-probe
+                const uint64_t inc = wave_ballot(flag == 2);
+                const uint64_t missing = wave_ballot(flag == 0);
+                const uint64_t upto = inc ? (inc & (~inc + 1)) * 2 - 1 : ~0ull;
+                if (missing & upto) {
+                    __builtin_amdgcn_s_sleep(2);
                     continue;
                 }
                 unsigned long long part = ((upto >> lane) & 1) ? val : 0ull;
 #pragma unroll
                 for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
                 excl += part;
-                if (incl) break;
+                if (inc) break;
                 top -= 64;
             }
             if (lane == 0)
-                __hip_atomic_store(&st[task], lb_pack(P.epoch, 2, excl + total),
+                __hip_atomic_store(&P.state[g], lb_pack(P.epoch, 2, excl + total),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (lane == 0) {
-            if (band == 0) P.frame_offsets[frame] = excl;
-            if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = excl + total;
-            sm.misc[1] = (uint32_t)excl;
-            sm.misc[3] = (uint32_t)(excl >> 32);
-        }
-    } else if (tid == 0) {
-        sm.misc[1] = 0;
-        sm.misc[3] = 0;
+        if (lane == 0) s_base = excl;
     }
     __syncthreads();
-    unsigned long long out_idx =
-        (((unsigned long long)sm.misc[3] << 32) | sm.misc[1]) + excl_in_band;
+    const unsigned long long base = s_base;
+    if (task < P.ntasks) {
+        const uint32_t frame = task / P.bands_per_frame;
+        const uint32_t band = task - frame * P.bands_per_frame;
+        if (band == 0) P.frame_offsets[frame] = base + s_task_off[tid];
+        if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = base + s_task_off[tid] + cnt;
+    }
 
-    // ---- expand keep-bits into raster-ordered points
-    if (P.flags & kFlagNoEmit) return;
-    for (uint32_t w = w_lo; w < w_hi; ++w) {
-        uint32_t bits = sm.bitmap[w];
-        const uint32_t r = w / nw;
-        const uint32_t xb = (w - r * nw) * 32;
-        const uint32_t y = y0 + r;
-        while (bits) {
-            const uint32_t b = __builtin_ctz(bits);
-            bits &= bits - 1;
-            if (out_idx < P.cap) P.out[out_idx] = make_uint2(xb + b, y);
-            ++out_idx;
+    // copy: wave w handles tasks w, w+4, ... of the group
+    const uint32_t ntask_here = min((uint32_t)kCompactTasks, P.ntasks - g * kCompactTasks);
+    const uint32_t slot_pts = P.slot_bytes / 8;
+    for (uint32_t i = wave; i < ntask_here; i += kCompactTasks / 64) {
+        const uint32_t tk = g * kCompactTasks + i;
+        const uint32_t n = P.counts[tk];
+        if (n == 0) continue;
+        const unsigned long long off = base + s_task_off[i];
+        const uint8_t* slot = P.slots + (uint64_t)tk * P.slot_bytes;
+        if (n <= slot_pts) {
+            const uint2* src = reinterpret_cast<const uint2*>(slot);
+            for (uint32_t k = lane; k < n; k += 64)
+                if (off + k < P.cap) P.out[off + k] = src[k];
+        } else {
+            // dense band: expand its bitmap, 64 words per round, in raster order
+            const uint32_t frame = tk / P.bands_per_frame;
+            const uint32_t band = tk - frame * P.bands_per_frame;
+            const uint32_t y0 = 3 + band * P.rows;
+            const uint32_t rows = min(P.rows, P.height - 3 - y0);
+            const uint32_t nwords = rows * P.words_per_row;
+            const uint32_t* words = reinterpret_cast<const uint32_t*>(slot);
+            unsigned long long o = off;
+            for (uint32_t w0 = 0; w0 < nwords; w0 += 64) {
+                const uint32_t w = w0 + lane;
+                uint32_t bits = w < nwords ? words[w] : 0u;
+                const uint32_t c = __popc(bits);
+                uint32_t inc = c;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t v = __shfl_up(inc, d, 64);
+                    if (lane >= (uint32_t)d) inc += v;
+                }
+                unsigned long long k = o + inc - c;
+                const uint32_t r = w / P.words_per_row;
+                const uint32_t xb = (w - r * P.words_per_row) * 32;
+                while (bits) {
+                    const uint32_t bit = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    if (k < P.cap) P.out[k] = make_uint2(xb + bit, y0 + r);
+                    ++k;
+                }
+                o += __shfl(inc, 63, 64);
+            }
         }
     }
 }
@@ -563,13 +684,17 @@ static BandKernelFn pick(uint32_t nms, uint32_t n) {
     }
 }
 
-hipError_t launch_band_kernel(const BandParams& p, uint32_t nms, uint32_t n,
-                              hipStream_t stream) {
+hipError_t launch_detect(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
+                         hipStream_t stream) {
     BandKernelFn fn = pick(nms, n);
     if (!fn) return hipErrorInvalidValue;
-    const LdsLayout L = make_layout(p.rows, p.words_per_row, nms != kNmsOff);
+    const LdsLayout L = make_layout(p.rows, p.words_per_row, score_bytes_for(nms));
     if (L.total > kMaxLds) return hipErrorInvalidValue;
     hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint32_t ngroups = (c.ntasks + kCompactTasks - 1) / kCompactTasks;
+    hipLaunchKernelGGL(compact_kernel, dim3(ngroups), dim3(kCompactTasks), 0, stream, c);
     return hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--variants", default="maxt:0,maxt:1,maxt:3,off:0,off:3,sad:0")
+    ap.add_argument("--variants", default="maxt:0,maxt:2,maxt:3,off:0,off:2,off:3,sad:0")
     args = ap.parse_args()
     import torch
 
