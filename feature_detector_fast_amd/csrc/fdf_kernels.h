@@ -26,6 +26,8 @@ constexpr int kCompactTasks = 256;            // tasks per workgroup of the comp
 // variable by the host layer; never part of the C ABI.  Results are wrong when set.
 constexpr uint32_t kFlagNoFullTest = 1;   // candidates are never tested (no keypoints)
 constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (counts only)
+constexpr uint32_t kFlagNoPrefilter = 4;  // skip the per-group pre-filter loop
+constexpr uint32_t kFlagNoLoad = 8;       // skip the global->LDS tile loads
 
 struct LdsLayout {
     uint32_t tile, scores, bitmap, gq_item, gq_cand, pq, kp_list, misc, total;

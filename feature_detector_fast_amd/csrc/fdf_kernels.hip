@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         __syncthreads();   // previous chunk's readers are done with the tile
         // ---- stage tile rows [tr_lo, tr_hi) x columns [X0-16, X0+kChunk+16) into LDS
         constexpr uint32_t kVecPerRow = kPitch / 16;
-        const uint32_t nvec = (tr_hi - tr_lo) * kVecPerRow;
+        const uint32_t nvec = (P.flags & kFlagNoLoad) ? 0u : (tr_hi - tr_lo) * kVecPerRow;
         for (uint32_t v = tid; v < nvec; v += kThreads) {
             const uint32_t tr = tr_lo + v / kVecPerRow;
             const uint32_t tv = v % kVecPerRow;
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         const uint32_t g_lo = (uint32_t)(need_lo - ((int)X0 - 4)) >> 2;
         const uint32_t g_hi = ((uint32_t)(need_hi - ((int)X0 - 4)) >> 2) + 1;
         const uint32_t ng = g_hi - g_lo;
-        const uint32_t nitems = (s_hi - s_lo) * ng;
+        const uint32_t nitems = (P.flags & kFlagNoPrefilter) ? 0u : (s_hi - s_lo) * ng;
         const ChunkCtx cc{t, X0, rows, nw};
 
         uint32_t* gqi = sm.gq_item + wave * kGroupQ;

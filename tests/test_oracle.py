@@ -1,0 +1,212 @@
+"""CPU tests of the checker itself: the scalar oracle (oracle/fast_oracle.c) must reproduce
+the reference's golden vectors and unit-test KATs before anything is compared against it;
+the AVX2 port (the CPU baseline) must agree with the oracle; and the algebraic
+reformulations the HIP kernels rely on are verified here in numpy on the same ground."""
+import numpy as np
+import pytest
+
+import workloads
+from oracle import oracle
+
+CIRCLE = ((0, -3), (1, -3), (2, -2), (3, -1), (3, 0), (3, 1), (2, 2), (1, 3),
+          (0, 3), (-1, 3), (-2, 2), (-3, 1), (-3, 0), (-3, -1), (-2, -2), (-1, -3))
+
+
+# --- golden vectors (tests/golden/, decoded from the reference's media/ overlays) ---------
+
+def test_golden_nms_off(golden):
+    img, off, _ = golden
+    assert np.array_equal(oracle.detect(img, 16, 9, 0), off)
+    assert len(off) == 309
+
+
+def test_golden_max_threshold(golden):
+    img, _, maxt = golden
+    assert np.array_equal(oracle.detect(img, 16, 9, 1), maxt)
+    assert len(maxt) == 131
+
+
+@pytest.mark.parametrize("t,n,nms,count", [(16, 9, 2, 135), (16, 12, 2, 80), (32, 12, 2, 16),
+                                           (16, 12, 1, 77), (8, 12, 2, 318)])
+def test_survey_cross_check_counts(golden, t, n, nms, count):
+    """Counts measured by the survey's independent restatement."""
+    assert len(oracle.detect(golden[0], t, n, nms)) == count
+
+
+# --- KATs from the reference's unit tests -------------------------------------------------
+
+HAND_RING = [37, 37, 39, 39, 37, 42, 43, 16, 14, 13, 15, 16, 15, 38, 37, 38]
+
+
+def test_47_115_score_kat():
+    """src/fast_simd.rs:919-948: centre 17 with this ring, n=9 -> max-t score 20."""
+    assert oracle.score_max_threshold(17, HAND_RING, 9) == 20
+    assert oracle.is_corner(17, HAND_RING, 16, 9)
+
+
+def test_47_115_hand_detect():
+    """src/fast_simd.rs:950-1022: the 128x128 sample image has a keypoint at (64, 64)."""
+    img = np.zeros((128, 128), dtype=np.uint8)
+    img[64, 64] = 17
+    for (dx, dy), v in zip(CIRCLE, HAND_RING):
+        img[64 + dy, 64 + dx] = v
+    assert [64, 64] in oracle.detect(img, 16, 9, 0).tolist()
+
+
+def _consecutive(z, k):
+    """src/opencv_compat.rs:311-325 (the helper under test there)."""
+    n = len(z)
+    for s in range(n):
+        run = 0
+        for i in range(n):
+            if not z[(s + i) % n]:
+                break
+            run += 1
+        if run >= k:
+            return True
+    return False
+
+
+def test_consecutive_kats():
+    """src/opencv_compat.rs:327-345 verbatim vectors."""
+    assert not _consecutive([0, 0, 0, 1], 3)
+    assert not _consecutive([1, 0, 0, 1], 3)
+    assert _consecutive([1, 0, 1, 1], 2)
+    assert _consecutive([0, 1, 1, 1], 3)
+    assert _consecutive([1, 0, 1, 1], 3)
+    assert _consecutive([1, 1, 0, 1], 3)
+    assert _consecutive([1, 1, 1, 0], 3)
+    assert not _consecutive([1, 0, 0, 0, 1, 0, 0, 1, 0, 0, 1, 0, 0, 1], 3)
+    assert _consecutive([1, 0, 0, 0, 1, 0, 0, 1, 0, 0, 1, 1, 1, 1], 4)
+
+
+def test_oracle_corner_matches_cyclic_helper():
+    """The oracle's run test equals the KAT helper on random rings (n = 9..16)."""
+    rng = np.random.default_rng(0)
+    for _ in range(3000):
+        ring = rng.integers(0, 256, 16).tolist()
+        c = int(rng.integers(0, 256))
+        t = int(rng.integers(0, 80))
+        n = int(rng.integers(9, 17))
+        bright = [p > c + t for p in ring]
+        dark = [p < c - t for p in ring]
+        want = _consecutive(bright, n) or _consecutive(dark, n)
+        assert oracle.is_corner(c, ring, t, n) == want
+
+
+def test_sad_score_against_formula():
+    """src/fast_simd.rs:1185-1236 (test_score_function_3), on 200k random triples."""
+    rng = np.random.default_rng(0)
+    for _ in range(20000):
+        ring = rng.integers(0, 256, 16)
+        c = int(rng.integers(0, 256))
+        t = int(rng.integers(0, 256))
+        light = sum(int(c - p - t) for p in ring if c - p > t)
+        dark = sum(int(p - c - t) for p in ring if p - c > t)
+        assert oracle.score_sum_abs(c, ring.tolist(), t) == max(light, dark)
+
+
+# --- the kernels' algebra, checked on the CPU -------------------------------------------
+
+def test_max_threshold_equals_arc_strength():
+    """fast_band_kernel scores a keypoint as its arc strength (max_k min_w p - c, or the dark
+    mirror), which equals the reference's min(|eh|, |el|) whenever 9 <= n (windows intersect)."""
+    rng = np.random.default_rng(1)
+    checked = 0
+    while checked < 4000:
+        ring = rng.integers(0, 256, 16)
+        c = int(rng.integers(0, 256))
+        t = int(rng.integers(0, 60))
+        n = int(rng.integers(9, 17))
+        if not oracle.is_corner(c, ring.tolist(), t, n):
+            continue
+        dark = any(all(ring[(k + i) % 16] < c - t for i in range(n)) for k in range(16))
+        q = 255 - ring if dark else ring
+        cq = 255 - c if dark else c
+        best = max(min(q[(k + i) % 16] for i in range(n)) for k in range(16))
+        assert best - cq == oracle.score_max_threshold(c, ring.tolist(), n)
+        checked += 1
+
+
+def _lerp(a, b, r):
+    return (a.astype(np.int32) + b.astype(np.int32) + r) >> 1
+
+
+def test_lerp_byte_comparisons_exact():
+    """The pre-filter's v_lerp_u8 comparisons equal X - c > t and X - c < -t for all
+    (c, X, t < 255) -- the constants are the ones lerp_consts() computes."""
+    c = np.arange(256)[:, None]
+    x = np.arange(256)[None, :]
+    for t in range(255):
+        ob, od = t & 1, (t + 1) & 1
+        kb = 128 - ((t + ob) >> 1)
+        kd = 255 - ((254 - t + od) >> 1)
+        bright = _lerp(_lerp(x, 255 - c, ob), np.full((256, 256), kb), 0) >= 128
+        not_dark = _lerp(_lerp(x, 255 - c, od), np.full((256, 256), kd), 0) >= 128
+        assert np.array_equal(bright, x > c + t), t
+        assert np.array_equal(~not_dark, x < c - t), t
+
+
+def _prefilter(ring, c, t, n):
+    card = [ring[0], ring[4], ring[8], ring[12]]
+    b = [p > c + t for p in card]
+    d = [p < c - t for p in card]
+    if n < 12:
+        return ((b[0] or b[2]) and (b[1] or b[3])) or ((d[0] or d[2]) and (d[1] or d[3]))
+    return sum(b) >= 3 or sum(d) >= 3
+
+
+def test_prefilter_is_necessary():
+    """Every keypoint passes the (reformulated) cardinal pre-filter of src/fast_simd.rs:441-509."""
+    rng = np.random.default_rng(2)
+    for _ in range(20000):
+        ring = rng.integers(0, 256, 16).tolist()
+        c = int(rng.integers(0, 256))
+        t = int(rng.integers(0, 60))
+        n = int(rng.integers(9, 17))
+        if oracle.is_corner(c, ring, t, n):
+            assert _prefilter(ring, c, t, n)
+
+
+# --- error semantics ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("w,h,n,expect", [
+    (10, 2, 9, ("err", oracle.ERR_SIZE)), (0, 0, 9, ("err", oracle.ERR_SIZE)),
+    (0, 3, 9, ("empty",)), (100, 6, 9, ("empty",)), (5, 7, 9, ("err", oracle.ERR_SIZE)),
+    (6, 7, 9, ("empty",)), (7, 7, 9, ("ok",)), (10, 10, 8, ("err", oracle.ERR_COUNT)),
+    (10, 10, 17, ("err", oracle.ERR_COUNT))])
+def test_reference_size_rules(w, h, n, expect):
+    status, empty = oracle.check(w, h, n, 0)
+    if expect[0] == "err":
+        assert status == expect[1]
+    else:
+        assert status == 0 and empty == (expect[0] == "empty")
+
+
+# --- the AVX2 port (CPU baseline) agrees with the oracle ---------------------------------
+
+@pytest.mark.parametrize("nms", [0, 1, 2])
+def test_avx2_port_matches_oracle(golden, nms):
+    rng = np.random.default_rng(10 + nms)
+    imgs = [golden[0], rng.integers(0, 256, (37, 91), dtype=np.uint8),
+            workloads.s2_frame(1, 200, 120), workloads.s1_frame(2, 333, 77)]
+    for img in imgs:
+        for t, n in ((16, 9), (8, 12), (30, 16), (0, 10)):
+            assert np.array_equal(oracle.avx2_detect(img, t, n, nms),
+                                  oracle.detect(img, t, n, nms)), (img.shape, t, n, nms)
+
+
+# --- synthetic workload generators (SURVEY.md §8d counts) --------------------------------
+
+def test_s1_1080p_counts():
+    img = workloads.s1_frame(0)
+    assert img.shape == (1080, 1920)
+    assert len(oracle.detect(img, 16, 9, 0)) == 10346
+    assert len(oracle.detect(img, 16, 9, 1)) == 4332
+
+
+def test_s2_1080p_counts():
+    img = workloads.s2_frame(0)
+    assert len(oracle.detect(img, 16, 9, 0)) == 30877
+    assert len(oracle.detect(img, 16, 9, 1)) == 5426
+    assert len(oracle.detect(img, 16, 12, 0)) == 0
