@@ -216,6 +216,7 @@ __device__ __forceinline__ void test_pixels(const Smem<ScoreT>& sm, const uint32
 #pragma unroll
     for (int i = 0; i < 16; ++i) bright[i] = wave_ballot((int)p[i] > upper) & active;
     const uint64_t kb = arc_test<N>(bright);
+    __builtin_amdgcn_sched_barrier(0);   // keep the two polarities' 32 masks from co-residing
 #pragma unroll
     for (int i = 0; i < 16; ++i) dark[i] = wave_ballot((int)p[i] < lower) & active;
     const uint64_t kd = arc_test<N>(dark);
@@ -271,7 +272,8 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
     const LdsLayout L = make_layout(P.rows, P.words_per_row, score_bytes_for(NMS));
     const Smem<ScoreT> sm = carve<ScoreT>(smem_raw, L);
     const uint32_t tid = threadIdx.x;
-    const uint32_t wave = tid >> 6;
+    // wave index as a provably wave-uniform (SGPR) value: loops bounded by it stay uniform
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
     const uint32_t W = P.width, H = P.height, nw = P.words_per_row, t = P.threshold;
 
@@ -341,7 +343,19 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         const uint32_t g_lo = (uint32_t)(need_lo - ((int)X0 - 4)) >> 2;
         const uint32_t g_hi = ((uint32_t)(need_hi - ((int)X0 - 4)) >> 2) + 1;
         const uint32_t ng = g_hi - g_lo;
-        const uint32_t nitems = (P.flags & kFlagNoPrefilter) ? 0u : (s_hi - s_lo) * ng;
+        // item rows: score rows whose image row is a centre row (3 <= y < H-3); ring rows
+        // outside the centre domain only need zero scores
+        const uint32_t si_lo = max(s_lo, y0 < 4 ? 4 - y0 : 0u);
+        const uint32_t si_hi = min(s_hi, H - 2 - y0);
+        const uint32_t nitems =
+            (P.flags & kFlagNoPrefilter) || si_hi <= si_lo ? 0u : (si_hi - si_lo) * ng;
+        if constexpr (NMS != kNmsOff) {
+            for (uint32_t ss = s_lo; ss < s_hi; ++ss) {
+                if (ss >= si_lo && ss < si_hi) continue;
+                for (uint32_t k = tid; k < kScorePitch; k += kThreads)
+                    sm.scores[ss * kScorePitch + k] = 0;
+            }
+        }
         const ChunkCtx cc{t, X0, rows, nw};
 
         uint32_t* gqi = sm.gq_item + wave * kGroupQ;
@@ -349,38 +363,42 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
         uint32_t* pq = sm.pq + wave * kPixelQ;
         uint32_t gcount = 0, pcount = 0;
         const bool no_test = (P.flags & kFlagNoFullTest) != 0;
-        // this lane's first item, then advance by kThreads items per round
+        const bool col_edges = X0 < 4 || X0 + kChunk + 4 > W - 3;   // some group is clipped
+        // this lane's first item, then advance by kThreads items per round; `toff` tracks
+        // the tile offset of the group's first byte: (s + 3) * kPitch + 12 + 4 * gi
         uint32_t item = wave * 64 + lane;
-        uint32_t s = s_lo + item / ng;
+        uint32_t s = si_lo + item / ng;
         uint32_t gi = g_lo + item % ng;
+        uint32_t toff = (s + 3) * kPitch + 12 + 4 * gi;
         for (uint32_t base = wave * 64; base < nitems; base += kThreads) {
             uint32_t cand = 0;
             if (item < nitems) {
-                cand = prefilter_group<N>(sm.tile + (s + 3) * kPitch + 12 + 4 * gi, lk);
-                const int y = (int)y0 - 1 + (int)s;
-                const int x0 = (int)X0 - 4 + 4 * (int)gi;
-                if (y < 3 || y >= (int)H - 3) cand = 0;
-                if (x0 < 3 || x0 + 4 > (int)W - 3) {
-                    uint32_t vm = 0;
+                cand = prefilter_group<N>(sm.tile + toff, lk);
+                if (col_edges) {
+                    const int x0 = (int)X0 - 4 + 4 * (int)gi;
+                    if (x0 < 3 || x0 + 4 > (int)W - 3) {
+                        uint32_t vm = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (x0 + j >= 3 && x0 + j < (int)W - 3) vm |= 0x80u << (8 * j);
-                    cand &= vm;
+                        for (int j = 0; j < 4; ++j)
+                            if (x0 + j >= 3 && x0 + j < (int)W - 3) vm |= 0x80u << (8 * j);
+                        cand &= vm;
+                    }
                 }
                 if constexpr (NMS != kNmsOff) {
-                    ScoreT* sp = sm.scores + s * kScorePitch + 4 * gi;
+                    // score (s, 4gi) = s * kScorePitch + 4 gi = toff - 3 kPitch - 12 - 16 s
+                    ScoreT* sp = sm.scores + (toff - 3 * kPitch - 12 - (s << 4));
                     if constexpr (sizeof(ScoreT) == 1) *reinterpret_cast<uint32_t*>(sp) = 0;
                     else *reinterpret_cast<uint2*>(sp) = make_uint2(0, 0);
                 }
             }
-            const bool has = cand != 0 && !no_test;
-            const uint64_t bal = wave_ballot(has);
-            if (has) {
+            const uint64_t bal = wave_ballot(cand != 0);
+            if (cand != 0) {
                 const uint32_t pos = gcount + lanes_below(bal);
                 gqi[pos] = (s << 12) | gi;
                 gqc[pos] = cand;
             }
             gcount += (uint32_t)__popcll(bal);
+            if (no_test) gcount = 0;
             while (gcount >= 16) {
                 gcount -= 16;
                 pcount = expand_groups(gqi + gcount, gqc + gcount, 16, pq, pcount, lane);
@@ -391,7 +409,12 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
             }
             item += kThreads;
             gi += kThreads;
-            while (gi >= g_hi) { gi -= ng; ++s; }
+            toff += 4 * kThreads;
+            while (gi >= g_hi) {
+                gi -= ng;
+                ++s;
+                toff += kPitch - 4 * ng;
+            }
         }
         if (gcount > 0) pcount = expand_groups(gqi, gqc, gcount, pq, pcount, lane);
         while (pcount > 0) {
@@ -489,7 +512,8 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
     __shared__ uint32_t s_wave_sum[kCompactTasks / 64];
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_group;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t ngroups = (P.ntasks + kCompactTasks - 1) / kCompactTasks;
     if (tid == 0) {   // groups in dispatch order: a group's predecessors are resident or done
         const uint32_t g = atomicAdd(P.ticket, 1u);
