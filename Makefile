@@ -15,13 +15,16 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude
 
 all: $(LIBFDF) oracle/liboracle.so oracle/libfast_avx2.so tests/cpp/test_cpp_api
 
-$(CSRC)/fdf_kernels.o: $(CSRC)/fdf_kernels.hip $(CSRC)/fdf_kernels.h
+$(CSRC)/fdf_kernels.o: $(CSRC)/fdf_kernels.hip $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/fdf_sweep.o: $(CSRC)/fdf_sweep.hip $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/fdf_api.o: $(CSRC)/fdf_api.cpp $(CSRC)/fdf_kernels.h include/fdf.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_api.o
+$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle/liboracle.so: oracle/fast_oracle.c oracle/fast_oracle.h

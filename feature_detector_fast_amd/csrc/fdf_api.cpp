@@ -75,15 +75,46 @@ int ensure(T** buf, size_t* have, size_t need, bool zero, hipStream_t stream) {
     return FDF_OK;
 }
 
-// Band height: tall bands amortise the 8-row halo; short bands fill the 256 CUs when the
-// whole job is small (e.g. one frame).  Capped so the LDS layout fits.
-uint32_t pick_rows(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score_bytes) {
+// Band geometry of the sweep kernel.  A band is R full-width centre rows; its 4 waves take
+// units = column strips (992 centres) x sub-bands.  Tall bands amortise the 8-row halo of a
+// sub-band; short bands give a small job (one frame) enough workgroups.  The LDS footprint
+// is kept <= 40 KB so 4 workgroups fit a CU.
+struct Geometry {
+    uint32_t R, nstrips, nsub;
+};
+
+uint32_t gcd(uint32_t a, uint32_t b) { return b ? gcd(b, a % b) : a; }
+
+Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score_bytes) {
+    Geometry g;
+    g.nstrips = (w - 3 + fdfk::kStripCols - 1) / fdfk::kStripCols;
+    g.nsub = 4 / gcd(g.nstrips, 4);                    // units a multiple of the 4 waves
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
-    uint32_t R = 8;
-    if ((uint64_t)n_frames * ((centre_rows + 7) / 8) < 1024) R = 4;
-    while (R > 1 && fdfk::make_layout(R, nw, score_bytes).total > fdfk::kMaxLds) --R;
-    return R;
+    // LDS per workgroup sets the workgroups per CU: 3 without NMS, 2 for max-threshold,
+    // SAD's 16-bit score ring leaves room for 1.
+    uint32_t budget = score_bytes == 0 ? 53 * 1024 : (score_bytes == 1 ? 80 * 1024 : fdfk::kSweepMaxLds);
+    if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
+    // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
+    // the most owned rows per sweep step; a grid that cannot fill the chip takes the
+    // shortest sweep (one 8-step block per unit) for the lowest latency.
+    double best = -1.0;
+    g.R = 0;
+    for (uint32_t R = g.nsub; R <= 256 && R < centre_rows + g.nsub; R += g.nsub) {
+        if (fdfk::make_sweep_layout(R, nw, score_bytes).total > budget) break;
+        const uint64_t tasks = (uint64_t)n_frames * ((centre_rows + R - 1) / R);
+        if (tasks < 1024) break;
+        const uint32_t steps = fdfk::sweep_steps(R / g.nsub, score_bytes);
+        const double eff = (double)R / (double)(steps * g.nsub);
+        if (eff > best + 1e-9) { best = eff; g.R = R; }
+    }
+    if (g.R == 0) {
+        const uint32_t unit = 8 - 3 - (score_bytes ? 2 : 0);
+        g.R = g.nsub * unit;
+        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, score_bytes).total > budget)
+            g.R -= g.nsub;
+    }
+    return g;
 }
 
 // Enqueue detection + compaction over `n_frames` device frames (w, h >= 7).
@@ -91,9 +122,10 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream) {
     const uint32_t sb = fdfk::score_bytes_for(cfg->nms);
-    const uint32_t R = pick_rows(n_frames, w, h, sb);
+    const Geometry geo = pick_geometry(n_frames, w, h, sb);
+    const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
-    if (fdfk::make_layout(R, nw, sb).total > fdfk::kMaxLds) return FDF_ERR_SIZE;
+    if (fdfk::make_sweep_layout(R, nw, sb).total > fdfk::kSweepMaxLds) return FDF_ERR_SIZE;
     const uint32_t bands = (h - 6 + R - 1) / R;
     const uint64_t ntasks = (uint64_t)bands * n_frames;
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
@@ -130,6 +162,8 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.slots = ctx->d_slots;
     p.counts = ctx->d_counts;
     p.flags = dbg ? (uint32_t)std::strtoul(dbg, nullptr, 0) : 0u;
+    p.nstrips = geo.nstrips;
+    p.nsub = geo.nsub;
     fdfk::CompactParams c;
     c.width = w;
     c.height = h;
@@ -146,7 +180,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.frame_offsets = d_offsets;
     c.state = ctx->d_state;
     c.ticket = ctx->d_ticket;
-    if (fdfk::launch_detect(p, c, cfg->nms, cfg->count, stream) != hipSuccess)
+    if (fdfk::launch_sweep(p, c, cfg->nms, cfg->count, stream) != hipSuccess)
         return FDF_ERR_DEVICE;
     return FDF_OK;
 }

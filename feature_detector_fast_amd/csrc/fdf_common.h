@@ -1,0 +1,150 @@
+// fdf_common.h -- device helpers shared by the FAST kernels (fdf_kernels.hip, fdf_sweep.hip):
+// circle geometry, byte-SWAR comparisons, wave ballots, the bit-sliced arc test and the
+// two NMS score functions of the reference (iwanders/feature_detector_fast).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fdf_kernels.h"
+
+namespace fdfk {
+
+// ---------------------------------------------------------------------------------------
+// Circle geometry: src/fast_simd.rs:79-98 (index 0 = north, clockwise).
+// ---------------------------------------------------------------------------------------
+__host__ __device__ constexpr int circle_dx(int i) {
+    constexpr int dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    return dx[i];
+}
+__host__ __device__ constexpr int circle_dy(int i) {
+    constexpr int dy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
+    return dy[i];
+}
+
+constexpr uint32_t kHigh = 0x80808080u;
+
+__device__ __forceinline__ uint32_t lerp_u8(uint32_t a, uint32_t b, uint32_t r) {
+    return __builtin_amdgcn_lerp(a, b, r);
+}
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+// v_cmp straight into an SGPR pair (HIP's __ballot(int) round-trips the bool through a VGPR).
+__device__ __forceinline__ uint64_t wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Per-launch byte constants of the lerp comparisons (threshold t < 255).
+struct LerpConsts {
+    uint32_t rb, kb, rd, kd;
+};
+__device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
+    LerpConsts k;
+    const uint32_t ob = t & 1u, od = (t + 1u) & 1u;
+    k.rb = ob * 0x01010101u;
+    k.kb = (128u - ((t + ob) >> 1)) * 0x01010101u;
+    k.rd = od * 0x01010101u;
+    k.kd = (255u - ((254u - t + od) >> 1)) * 0x01010101u;
+    return k;
+}
+
+// Cyclic run test on bit-sliced masks: bit k of b[i] = "lane k's circle pixel i qualifies".
+// Returns the lanes whose ring holds a run of >= N qualifying pixels (src/fast_simd.rs:247-295).
+template <int N>
+__device__ __forceinline__ uint64_t arc_test(const uint64_t (&b)[16]) {
+    uint64_t p2[16], p4[16], p8[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p2[i] = b[i] & b[(i + 1) & 15];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p4[i] = p2[i] & p2[(i + 2) & 15];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p8[i] = p4[i] & p4[(i + 4) & 15];
+    uint64_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) any |= p8[i] & p8[(i + N - 8) & 15];
+    return any;
+}
+
+// Per-lane form of the segment test (each lane tests its own pixel, all in VALU).
+// run_of: `m` holds the 16 circle flags twice (pixel i at bits i and i+16); true when some
+// cyclic run of >= N flags is set (src/fast_simd.rs:247-295).  Doubling ANDs as arc_test.
+template <int N>
+__device__ __forceinline__ bool run_of(uint32_t m) {
+    m &= m >> 1;
+    m &= m >> 2;
+    m &= m >> 4;
+    if constexpr (N > 8) m &= m >> (N - 8);
+    return (m & 0xffffu) != 0;
+}
+
+// Bit 7 of byte j of f[m] is the flag of circle pixel 4j + m -> the doubled circle mask.
+__device__ __forceinline__ uint32_t gather_flags(const uint32_t (&f)[4]) {
+    uint32_t x = ((f[0] >> 7) & 0x01010101u) | ((f[1] >> 6) & 0x02020202u) |
+                 ((f[2] >> 5) & 0x04040404u) | ((f[3] >> 4) & 0x08080808u);  // pixel 4j+m: bit 8j+m
+    x |= x >> 4;                                         // pixels 0..7 in byte 0, 8..15 in byte 2
+    return __builtin_amdgcn_perm(x, x, 0x02000200u);     // bytes [b0, b2, b0, b2]
+}
+
+// Bright / dark runs of >= N on the ring p (src/fast_simd.rs:115-297): the 16 bytes are
+// packed 4 per word (byte j of word m = pixel 4j + m) and compared with the exact lerp SWAR.
+template <int N>
+__device__ __forceinline__ void lane_segment_test(uint32_t c, const uint32_t (&p)[16],
+                                                  const LerpConsts& k, bool& bright, bool& dark) {
+    const uint32_t nc = ~(c * 0x01010101u);
+    uint32_t fb[4], fn[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t w = p[m] | (p[m + 4] << 8) | (p[m + 8] << 16) | (p[m + 12] << 24);
+        fb[m] = lerp_u8(lerp_u8(w, nc, k.rb), k.kb, 0);   // p - c > t
+        fn[m] = lerp_u8(lerp_u8(w, nc, k.rd), k.kd, 0);   // NOT(p - c < -t)
+    }
+    bright = run_of<N>(gather_flags(fb));
+    dark = run_of<N>(~gather_flags(fn));
+}
+
+// Max-threshold score of a keypoint (src/fast_simd.rs:623-718, scalar :172-209).  For
+// 9 <= N any two N-windows of the 16-ring intersect, so min(|eh|, |el|) equals the arc
+// strength of the keypoint's own polarity: bright -> max_k min_{w_k} p - c,
+// dark -> c - min_k max_{w_k} p.  Dark is mapped onto bright with p -> 255 - p.
+template <int N>
+__device__ __forceinline__ uint32_t score_max_threshold(uint32_t c, const uint32_t (&p)[16],
+                                                        bool dark) {
+    const uint32_t m = dark ? 0xffu : 0u;
+    uint32_t q[16], m3[16], m6[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) q[i] = p[i] ^ m;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m3[i] = min(min(q[i], q[(i + 1) & 15]), q[(i + 2) & 15]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m6[i] = min(m3[i], m3[(i + 3) & 15]);
+    // window [i, i+N) = [i, i+6) u [i+K, i+K+6) u [i+N-6, i+N), contiguous for K below
+    constexpr int K = N > 12 ? N - 12 : 0;
+    uint32_t best = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        best = max(best, min(min(m6[i], m6[(i + K) & 15]), m6[(i + N - 6) & 15]));
+    }
+    return best - (c ^ m);
+}
+
+// Sum-of-absolute-differences score (src/fast_simd.rs:722-749, scalar :278-299).
+__device__ __forceinline__ uint32_t score_sum_abs(uint32_t c, const uint32_t (&p)[16],
+                                                  uint32_t t) {
+    const int upper = (int)(c + t), lower = (int)c - (int)t;
+    uint32_t sb = 0, sd = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        sb += (uint32_t)max((int)p[i] - upper, 0);
+        sd += (uint32_t)max(lower - (int)p[i], 0);
+    }
+    return max(sb, sd);
+}
+
+__device__ __forceinline__ unsigned long long lb_pack(uint32_t epoch, uint32_t flag,
+                                                      unsigned long long value) {
+    return ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | value;
+}
+
+}  // namespace fdfk

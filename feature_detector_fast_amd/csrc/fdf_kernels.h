@@ -26,14 +26,51 @@ constexpr int kCompactTasks = 256;            // tasks per workgroup of the comp
 // variable by the host layer; never part of the C ABI.  Results are wrong when set.
 constexpr uint32_t kFlagNoFullTest = 1;   // candidates are never tested (no keypoints)
 constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (counts only)
-constexpr uint32_t kFlagNoPrefilter = 4;  // skip the per-group pre-filter loop
-constexpr uint32_t kFlagNoLoad = 8;       // skip the global->LDS tile loads
+constexpr uint32_t kFlagNoPrefilter = 4;  // skip the per-group pre-filter loop (sweep: units)
+constexpr uint32_t kFlagNoLoad = 8;       // band kernel: skip the tile loads; sweep: rows are
+                                          // streamed and compared but never pre-filtered
+
+// Column-sweep kernel (fdf_sweep.hip): per-wave LDS region + the band bitmap.
+constexpr int kStripCols = 992;               // centres per wave strip (62 lanes x 16 columns)
+constexpr int kSweepRing = 4;                 // NMS score ring rows per wave (power of two)
+constexpr int kSweepDataRows = 8;             // pixel-row ring per wave read by the full test
+constexpr int kSweepPrefetch = 8;             // rows loaded ahead of the sweep (register queue)
+constexpr int kSweepPixelQ = 128;             // queued candidate pixels per wave (63 + 64)
+constexpr int kSweepKpCap = 256;              // unfinalized NMS keypoints per wave
+constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per workgroup)
+
+struct SweepLayout {
+    uint32_t data, pq, ring, kp, wave_bytes, bitmap, total;
+};
+
+__host__ __device__ inline uint32_t align16(uint32_t v);
+
+__host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw,
+                                                         uint32_t score_bytes) {
+    SweepLayout L;
+    uint32_t o = 0;
+    L.data = o;     o += kSweepDataRows * 1024;
+    L.pq = o;       o += kSweepPixelQ * 4;
+    L.ring = o;     o += kSweepRing * 1024 * score_bytes;
+    L.kp = o;       o += score_bytes ? kSweepKpCap * 4 : 0;
+    L.wave_bytes = align16(o);
+    L.bitmap = 4 * L.wave_bytes;
+    L.total = L.bitmap + align16(R * nw * 4) + 64;
+    return L;
+}
+
+// Sweep steps a unit of `rows` owned rows takes: the pre-filtered rows (owned rows plus, with
+// NMS, one score row each side) and 3 rows of vertical look-ahead, in whole 8-step blocks.
+__host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t score_bytes) {
+    return (rows + 3 + (score_bytes ? 2 : 0) + 7) & ~7u;
+}
 
 struct LdsLayout {
     uint32_t tile, scores, bitmap, gq_item, gq_cand, pq, kp_list, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t v) { return (v + 15u) & ~15u; }
+
 
 // R = centre rows per band, nw = bitmap words per image row, score_bytes = 0 (no NMS),
 // 1 (max-threshold scores fit u8) or 2 (sum-of-absolute-differences scores need u16).
@@ -75,6 +112,7 @@ struct BandParams {
     uint8_t* slots;              // ntasks * slot_bytes
     uint32_t* counts;            // ntasks keypoint counts (band order = raster order)
     uint32_t flags;              // kFlag* ablation switches, 0 in production
+    uint32_t nstrips, nsub;      // sweep kernel: column strips x sub-bands per band
 };
 
 struct CompactParams {
@@ -89,6 +127,9 @@ struct CompactParams {
     uint32_t* ticket;                // zero between launches (self-resetting)
 };
 
+hipError_t launch_compact(const CompactParams& c, hipStream_t stream);
+hipError_t launch_sweep(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
+                        hipStream_t stream);
 hipError_t launch_detect(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
                          hipStream_t stream);
 hipError_t launch_score_points(const uint8_t* img, uint32_t width, const uint2* pts,

@@ -30,50 +30,10 @@
 
 #include <type_traits>
 
+#include "fdf_common.h"
 #include "fdf_kernels.h"
 
 namespace fdfk {
-
-// ---------------------------------------------------------------------------------------
-// Circle geometry: src/fast_simd.rs:79-98 (index 0 = north, clockwise).
-// ---------------------------------------------------------------------------------------
-__host__ __device__ constexpr int circle_dx(int i) {
-    constexpr int dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    return dx[i];
-}
-__host__ __device__ constexpr int circle_dy(int i) {
-    constexpr int dy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
-    return dy[i];
-}
-
-constexpr uint32_t kHigh = 0x80808080u;
-
-__device__ __forceinline__ uint32_t lerp_u8(uint32_t a, uint32_t b, uint32_t r) {
-    return __builtin_amdgcn_lerp(a, b, r);
-}
-__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
-    return __builtin_amdgcn_alignbyte(hi, lo, s);
-}
-// v_cmp straight into an SGPR pair (HIP's __ballot(int) round-trips the bool through a VGPR).
-__device__ __forceinline__ uint64_t wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
-__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-// Per-launch byte constants of the lerp comparisons (threshold t < 255).
-struct LerpConsts {
-    uint32_t rb, kb, rd, kd;
-};
-__device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
-    LerpConsts k;
-    const uint32_t ob = t & 1u, od = (t + 1u) & 1u;
-    k.rb = ob * 0x01010101u;
-    k.kb = (128u - ((t + ob) >> 1)) * 0x01010101u;
-    k.rd = od * 0x01010101u;
-    k.kd = (255u - ((254u - t + od) >> 1)) * 0x01010101u;
-    return k;
-}
 
 // Cardinal pre-filter of the 4 centres at `px` (tile address of the group's first byte).
 // Returns bit 7 of byte j set iff centre j passes (a necessary condition for a keypoint).
@@ -107,61 +67,6 @@ __device__ __forceinline__ uint32_t prefilter_group(const uint8_t* px, const Ler
         not_dark = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));   // >= 2 not dark
     }
     return (bright | ~not_dark) & kHigh;
-}
-
-// Cyclic run test on bit-sliced masks: bit k of b[i] = "lane k's circle pixel i qualifies".
-// Returns the lanes whose ring holds a run of >= N qualifying pixels (src/fast_simd.rs:247-295).
-template <int N>
-__device__ __forceinline__ uint64_t arc_test(const uint64_t (&b)[16]) {
-    uint64_t p2[16], p4[16], p8[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p2[i] = b[i] & b[(i + 1) & 15];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p4[i] = p2[i] & p2[(i + 2) & 15];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p8[i] = p4[i] & p4[(i + 4) & 15];
-    uint64_t any = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) any |= p8[i] & p8[(i + N - 8) & 15];
-    return any;
-}
-
-// Max-threshold score of a keypoint (src/fast_simd.rs:623-718, scalar :172-209).  For
-// 9 <= N any two N-windows of the 16-ring intersect, so min(|eh|, |el|) equals the arc
-// strength of the keypoint's own polarity: bright -> max_k min_{w_k} p - c,
-// dark -> c - min_k max_{w_k} p.  Dark is mapped onto bright with p -> 255 - p.
-template <int N>
-__device__ __forceinline__ uint32_t score_max_threshold(uint32_t c, const uint32_t (&p)[16],
-                                                        bool dark) {
-    const uint32_t m = dark ? 0xffu : 0u;
-    uint32_t q[16], m3[16], m6[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) q[i] = p[i] ^ m;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m3[i] = min(min(q[i], q[(i + 1) & 15]), q[(i + 2) & 15]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m6[i] = min(m3[i], m3[(i + 3) & 15]);
-    // window [i, i+N) = [i, i+6) u [i+K, i+K+6) u [i+N-6, i+N), contiguous for K below
-    constexpr int K = N > 12 ? N - 12 : 0;
-    uint32_t best = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        best = max(best, min(min(m6[i], m6[(i + K) & 15]), m6[(i + N - 6) & 15]));
-    }
-    return best - (c ^ m);
-}
-
-// Sum-of-absolute-differences score (src/fast_simd.rs:722-749, scalar :278-299).
-__device__ __forceinline__ uint32_t score_sum_abs(uint32_t c, const uint32_t (&p)[16],
-                                                  uint32_t t) {
-    const int upper = (int)(c + t), lower = (int)c - (int)t;
-    uint32_t sb = 0, sd = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        sb += (uint32_t)max((int)p[i] - upper, 0);
-        sd += (uint32_t)max(lower - (int)p[i], 0);
-    }
-    return max(sb, sd);
 }
 
 template <typename ScoreT>
@@ -502,11 +407,6 @@ __global__ __launch_bounds__(kThreads) void fast_band_kernel(BandParams P) {
 // ---------------------------------------------------------------------------------------
 // Compaction: raster-order prefix over band counts, then slot -> final position copy.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ unsigned long long lb_pack(uint32_t epoch, uint32_t flag,
-                                                      unsigned long long value) {
-    return ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | value;
-}
-
 __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P) {
     __shared__ uint32_t s_task_off[kCompactTasks];
     __shared__ uint32_t s_wave_sum[kCompactTasks / 64];
@@ -717,6 +617,10 @@ hipError_t launch_detect(const BandParams& p, const CompactParams& c, uint32_t n
     hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    return launch_compact(c, stream);
+}
+
+hipError_t launch_compact(const CompactParams& c, hipStream_t stream) {
     const uint32_t ngroups = (c.ntasks + kCompactTasks - 1) / kCompactTasks;
     hipLaunchKernelGGL(compact_kernel, dim3(ngroups), dim3(kCompactTasks), 0, stream, c);
     return hipGetLastError();

@@ -1,0 +1,502 @@
+// fdf_sweep.hip -- column-sweep FAST-9..16 kernel for MI355X (gfx950), the production path.
+//
+// Replaces detect<NONMAX>() (iwanders/feature_detector_fast src/fast_simd.rs:301-620) with
+// determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
+//
+// One workgroup (4 waves) owns a band of R full-width centre rows of one frame.  The band is
+// cut into units = (column strip of 992 centres) x (sub-band of rows); a wave sweeps a unit
+// top to bottom:
+//   * lane l owns 16 columns (one 16-B buffer load per row); lanes 0 and 63 are halo lanes
+//     that only feed their neighbours, so a strip covers 62 x 16 = 992 centres;
+//   * pixel rows stream through an 8-deep register queue (loads run 8 rows ahead, never
+//     guarded by a branch, so the prefetch stays in flight), then into a per-wave LDS ring of
+//     the last 8 rows that the full test reads;
+//   * every pairwise comparison is made once and used by both of its pixels: the vertical
+//     pair (I(y), I(y+3)) gives S-flags for row y and N-flags for row y+3, the horizontal
+//     pair (I(x), I(x+3)) gives E-flags for x and W-flags for x+3 (a 3-byte shift, with the
+//     neighbouring lane's bytes via DPP).  Comparisons are byte-SWAR v_lerp_u8 (exact per
+//     byte, see fdf_common.h), so the cardinal pre-filter (src/fast_simd.rs:441-509) costs
+//     32 lerps per 16 pixels instead of 64;
+//   * candidate pixels go straight into a per-wave queue (one per lane per round) and are
+//     tested 64 at a time, one pixel per lane, with the VALU segment test of fdf_common.h on
+//     bytes read from the LDS ring (no global loads outside the row stream); every 2 rows
+//     the queue is drained, since the ring is about to drop the oldest row;
+//   * NMS: scores live in a 4-row LDS ring per wave; every 2 rows the queue is flushed and
+//     the keypoints of the finished rows pass the 3x3 strict-max test (:589-616) into the
+//     workgroup's band bitmap.
+// The band's keep-bits are then written to its output slot exactly as fdf_kernels.hip's
+// band kernel does, and compact_kernel orders all slots in raster order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "fdf_common.h"
+#include "fdf_kernels.h"
+
+namespace fdfk {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// DPP whole-wave shifts (GFX9 encodings): lane i reads lane i+1 / lane i-1; the lane that
+// falls off the wave reads 0 (it is a halo lane whose results are never used).
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, false);   // wave_shl:1
+}
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+}
+
+struct RowSource {
+    __amdgpu_buffer_rsrc_t rs;   // the frame; num_records = W * H + 15 (reads beyond return 0)
+    uint32_t W, H;
+};
+
+constexpr int kOutOfRange = 0x7ffffff0;   // a buffer offset past any frame: loads return 0
+
+// Bytes [xb, xb+16) of image row y: one 16-byte buffer load at any byte offset (gfx950
+// buffer loads need no alignment).  Branch-free, so the compiler's vmcnt bookkeeping keeps
+// the row prefetch in flight; rows outside the frame and negative offsets read 0.  Columns
+// outside [0, W) hold the neighbouring row's bytes -- only halo lanes and non-centre pixels
+// see them.
+__device__ __forceinline__ u32x4 load_row(const RowSource& src, int y, int xb) {
+    const int off = y * (int)src.W + xb;
+    const bool in = y >= 0 && y < (int)src.H && off >= 0;
+    return __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(src.rs, in ? off : kOutOfRange, 0, 0));
+}
+
+struct SweepShared {
+    uint8_t* data;         // kSweepDataRows x 1024 pixel bytes, slot (row - ys) & 7
+    uint32_t* pq;          // kSweepPixelQ: (row << 10) | strip column
+    void* ring;            // kSweepRing x 1024 scores (NMS)
+    uint32_t* kp;          // kSweepKpCap: (row << 10) | strip column
+    uint32_t* bitmap;      // band keep-bits, R x words_per_row
+};
+
+struct UnitCtx {
+    RowSource src;
+    uint32_t t, nw;
+    int S;                 // first owned centre column of the strip
+    int r0, r1;            // owned centre rows of the unit
+    int y0;                // first centre row of the band
+    int ys;                // first row of the unit's sweep (data ring slot 0)
+    uint32_t lane;
+    bool dense;            // NMS keypoint list overflowed: finalize densely
+    uint32_t pcount, kpn;
+    uint32_t flags;        // BandParams::flags (ablation runs only)
+};
+
+template <typename ScoreT>
+__device__ __forceinline__ ScoreT* ring_at(const SweepShared& sh, int y, int cl) {
+    return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kSweepRing - 1)) * 1024 + cl;
+}
+
+// Full test of `count` (<= 64) queued pixels from pq[0..count), one per lane (per-lane
+// VALU segment test, fdf_common.h).
+template <int NMS, int N, typename ScoreT>
+__device__ __forceinline__ void sweep_test(const SweepShared& sh, UnitCtx& u,
+                                           const LerpConsts& lk, const uint32_t* pq,
+                                           uint32_t count) {
+    const uint32_t lane = u.lane;
+    const bool act = lane < count;
+    const uint32_t code = act ? pq[lane] : 0u;
+    const int y = (int)(code >> 10), cl = (int)(code & 1023u);
+    const int x = u.S - 16 + cl;
+    // 7x7 neighbourhood from the LDS row ring: row y+dy in slot (y + dy - ys) & 7
+    const int rel = y - u.ys;
+    const uint8_t* d = sh.data + (act ? cl : 16);
+    uint32_t base[7];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) base[r] = (uint32_t)((rel + r - 3) & (kSweepDataRows - 1)) << 10;
+    uint32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = d[base[circle_dy(i) + 3] + circle_dx(i)];
+    const uint32_t c = d[base[3]];
+    bool kb, kd;
+    lane_segment_test<N>(c, p, lk, kb, kd);
+    const bool is_kp = act && (kb || kd);
+    const bool owned = cl >= 16 && cl < 16 + kStripCols && y >= u.r0 && y < u.r1;
+    if constexpr (NMS == kNmsOff) {
+        if (is_kp && owned)
+            atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
+    } else {
+        if (is_kp) {
+            const uint32_t score = NMS == kNmsMaxThreshold
+                                       ? score_max_threshold<N>(c, p, kd)
+                                       : score_sum_abs(c, p, u.t);
+            *ring_at<ScoreT>(sh, y, cl) = (ScoreT)score;
+        }
+        const bool add = is_kp && owned;
+        const uint64_t bal = wave_ballot(add);
+        if (add) {
+            const uint32_t k = u.kpn + lanes_below(bal);
+            if (k < kSweepKpCap) sh.kp[k] = code;
+        }
+        u.kpn += (uint32_t)__popcll(bal);
+    }
+}
+
+template <typename ScoreT>
+__device__ __forceinline__ bool nms_keep_ring(const SweepShared& sh, int y, int cl) {
+    const uint32_t v = *ring_at<ScoreT>(sh, y, cl);
+    const ScoreT* a = ring_at<ScoreT>(sh, y - 1, cl);
+    const ScoreT* m = ring_at<ScoreT>(sh, y, cl);
+    const ScoreT* b = ring_at<ScoreT>(sh, y + 1, cl);
+    return v > a[-1] && v > a[0] && v > a[1] && v > m[-1] && v > m[1] && v > b[-1] &&
+           v > b[0] && v > b[1];
+}
+
+// NMS: keep-bits for the unit's keypoints in rows <= ylim (all their neighbours scored).
+template <typename ScoreT>
+__device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u, int ylim,
+                                               int first_unfinal) {
+    const int H = (int)u.src.H;
+    if (u.kpn > kSweepKpCap) u.dense = true;
+    if (u.dense) {
+        // rare: the list overflowed -- scan the owned columns of the rows densely
+        const int lo = first_unfinal > u.r0 ? first_unfinal : u.r0;
+        for (int y = lo; y <= ylim && y < u.r1; ++y) {
+            if (y == 3 || y == H - 4) continue;
+            if (u.lane < 1 || u.lane > 62) continue;
+            for (int j = 0; j < 16; ++j) {
+                const int cl = (int)u.lane * 16 + j;
+                const int x = u.S - 16 + cl;
+                if (x < 3 || x >= (int)u.src.W - 3) continue;
+                if (*ring_at<ScoreT>(sh, y, cl) != 0 && nms_keep_ring<ScoreT>(sh, y, cl))
+                    atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
+            }
+        }
+        u.kpn = 0;
+        return;
+    }
+    uint32_t kept = 0;
+    for (uint32_t b0 = 0; b0 < u.kpn; b0 += 64) {
+        const uint32_t i = b0 + u.lane;
+        const bool act = i < u.kpn;
+        const uint32_t e = act ? sh.kp[i] : 0u;
+        const int y = (int)(e >> 10), cl = (int)(e & 1023u);
+        const bool fin = act && y <= ylim;
+        const bool carry = act && !fin;
+        const uint64_t bal = wave_ballot(carry);
+        if (carry) sh.kp[kept + lanes_below(bal)] = e;   // kept + idx <= i: read before write
+        kept += (uint32_t)__popcll(bal);
+        if (fin && y != 3 && y != H - 4 && nms_keep_ring<ScoreT>(sh, y, cl)) {
+            const int x = u.S - 16 + cl;
+            atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
+        }
+    }
+    u.kpn = kept;
+}
+
+// Test whatever is queued (a partial batch): the data ring is about to drop rows.
+template <int NMS, int N, typename ScoreT>
+__device__ __forceinline__ void sweep_drain(const SweepShared& sh, UnitCtx& u,
+                                            const LerpConsts& lk) {
+    if (u.pcount > 0 && !(u.flags & kFlagNoFullTest)) sweep_test<NMS, N, ScoreT>(sh, u, lk, sh.pq, u.pcount);
+    u.pcount = 0;
+}
+
+// Horizontal/vertical comparison flags of one row (bit 7 of each byte, 16 pixels).
+struct RowFlags {
+    u32x4 b, nd;
+};
+
+__device__ __forceinline__ RowFlags compare_rows(const u32x4& x, const u32x4& nc,
+                                                 const LerpConsts& k) {
+    RowFlags f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        f.b[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rb), k.kb, 0);   // x - c > t
+        f.nd[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rd), k.kd, 0);  // NOT(x - c < -t)
+    }
+    return f;
+}
+
+template <int NMS, int N>
+__device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
+    using ScoreT = typename std::conditional<NMS == kNmsSumAbsolute, uint16_t, uint8_t>::type;
+    const uint32_t lane = u.lane;
+    const int H = (int)u.src.H, W = (int)u.src.W;
+    const int xb = u.S - 16 + 16 * (int)lane;
+    // candidate columns of this lane: owned centres, plus for NMS the two border columns the
+    // strip's edge keypoints compare against (scores only)
+    u32x4 vmask;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int x = xb + 4 * m + j;
+            bool ok = x >= 3 && x < W - 3;
+            if (lane == 0) ok = ok && NMS != kNmsOff && x == u.S - 1;
+            if (lane == 63) ok = ok && NMS != kNmsOff && x == u.S + kStripCols;
+            if (ok) v |= 0x80u << (8 * j);
+        }
+        vmask[m] = v;
+    }
+    const int ringr = NMS == kNmsOff ? 0 : 1;
+    const int p0 = u.r0 - ringr, p1 = u.r1 + ringr;   // rows run through the pre-filter
+    const int ys = p0 - 3;                             // first row of vertical comparisons
+    const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
+    u.ys = ys;
+    u.pcount = 0;
+    u.kpn = 0;
+    u.dense = false;
+    int first_unfinal = u.r0;
+    u32x4* ring = reinterpret_cast<u32x4*>(sh.data) + lane;   // + slot * 64
+
+    // Prologue: rows ys..ys+2 straight to the LDS ring, rows ys+3..ys+10 into the queue.
+    u32x4 C[4];                                        // rows yv..yv+3, slot (row - ys) & 3
+    u32x4 Q[kSweepPrefetch];                           // row ys+k+3 (+8m) in slot (k+3) & 7
+#pragma unroll
+    for (int k = 0; k < 3; ++k) C[k] = load_row(u.src, ys + k, xb);
+#pragma unroll
+    for (int k = 0; k < kSweepPrefetch; ++k) Q[(k + 3) & 7] = load_row(u.src, ys + 3 + k, xb);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ring[k * 64] = C[k];
+    RowFlags V[4];                                     // vertical flags, slot (row-ys) & 3
+
+#define FDF_SWEEP_STEP(J)                                                                    \
+    {                                                                                        \
+        const int i = i0 + (J);                                                              \
+        const int yv = ys + i;                                                               \
+        const u32x4 s = Q[((J) + 3) & 7];                  /* row yv + 3 */                  \
+        ring[(((J) + 3) & 7) * 64] = s;                                                      \
+        Q[((J) + 3) & 7] = load_row(u.src, yv + 3 + kSweepPrefetch, xb);                     \
+        C[((J) + 3) & 3] = s;                                                                \
+        const u32x4 c = C[(J) & 3];                                                          \
+        const u32x4 nc = ~c;                                                                 \
+        V[(J) & 3] = compare_rows(s, nc, lk);                                                \
+        if (yv >= p0 && yv < p1 && !(u.flags & kFlagNoLoad)) {                               \
+            if constexpr (NMS != kNmsOff) {                                                  \
+                /* fresh ring row: scores default to 0 */                                    \
+                ScoreT* rp = ring_at<ScoreT>(sh, yv, 16 * (int)lane);                        \
+                if constexpr (sizeof(ScoreT) == 1) *reinterpret_cast<u32x4*>(rp) = u32x4{0, 0, 0, 0}; \
+                else { reinterpret_cast<u32x4*>(rp)[0] = u32x4{0, 0, 0, 0};                  \
+                       reinterpret_cast<u32x4*>(rp)[1] = u32x4{0, 0, 0, 0}; }                \
+            }                                                                                \
+            if (yv >= 3 && yv < H - 3) {                                                     \
+                u32x4 e;                                                                     \
+                e[0] = alignbyte(c[1], c[0], 3);                                             \
+                e[1] = alignbyte(c[2], c[1], 3);                                             \
+                e[2] = alignbyte(c[3], c[2], 3);                                             \
+                e[3] = alignbyte(from_next_lane(c[0]), c[3], 3);                             \
+                const RowFlags h = compare_rows(e, nc, lk);                                  \
+                const uint32_t pb = from_prev_lane(h.b[3]), pnd = from_prev_lane(h.nd[3]);   \
+                const RowFlags& vs = V[(J) & 3];                                             \
+                const RowFlags& vn = V[((J) + 1) & 3];                                       \
+                u32x4 cand;                                                                  \
+                _Pragma("unroll") for (int m = 0; m < 4; ++m) {                              \
+                    const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);          \
+                    const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);      \
+                    const uint32_t bn = ~vn.nd[m], bs = vs.b[m], be = h.b[m], bw = ~hndw;    \
+                    const uint32_t dn = ~vn.b[m], ds = vs.nd[m], de = h.nd[m], dw = ~hbw;    \
+                    uint32_t br, nd;                                                         \
+                    if constexpr (N < 12) {                                                  \
+                        br = (bn | bs) & (be | bw);                                          \
+                        nd = (dn & ds) | (de & dw);                                          \
+                    } else {                                                                 \
+                        br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                  \
+                        nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                \
+                    }                                                                        \
+                    cand[m] = (br | ~nd) & vmask[m];                                         \
+                }                                                                            \
+                /* candidate pixels straight into the pixel queue, one per lane per round: */\
+                /* column 4m + j of the lane at bit 8j + m */                                \
+                uint32_t cm = (cand[0] >> 7) | (cand[1] >> 6) | (cand[2] >> 5) | (cand[3] >> 4); \
+                for (;;) {                                                                   \
+                    const bool has = cm != 0;                                                \
+                    const uint64_t bal = wave_ballot(has);                                   \
+                    if (bal == 0) break;                                                     \
+                    if (has) {                                                               \
+                        const uint32_t b = (uint32_t)__builtin_ctz(cm);                      \
+                        const uint32_t col = 4 * (b & 7u) + (b >> 3);                        \
+                        sh.pq[u.pcount + lanes_below(bal)] =                                 \
+                            ((uint32_t)yv << 10) | (16 * lane + col);                        \
+                        cm &= cm - 1;                                                        \
+                    }                                                                        \
+                    u.pcount += (uint32_t)__popcll(bal);                                     \
+                    if (u.pcount >= 64) {                                                    \
+                        u.pcount -= 64;                                                      \
+                        if (!(u.flags & kFlagNoFullTest))                                    \
+                            sweep_test<NMS, N, ScoreT>(sh, u, lk, sh.pq + u.pcount, 64);     \
+                    }                                                                        \
+                }                                                                            \
+            }                                                                                \
+        }                                                                                    \
+        if (((J) & 1) == 0 && i >= 4) {                                                      \
+            /* rows <= yv are queued and the data ring holds yv-4..yv+3: test them all;      \
+               NMS finalizes rows <= yv-1 */                                                 \
+            sweep_drain<NMS, N, ScoreT>(sh, u, lk);                                          \
+            if constexpr (NMS != kNmsOff) {                                                  \
+                sweep_finalize<ScoreT>(sh, u, yv - 1, first_unfinal);                        \
+                first_unfinal = yv;                                                          \
+            }                                                                                \
+        }                                                                                    \
+    }
+
+    for (int i0 = 0; i0 < T; i0 += 8) {
+        FDF_SWEEP_STEP(0)
+        FDF_SWEEP_STEP(1)
+        FDF_SWEEP_STEP(2)
+        FDF_SWEEP_STEP(3)
+        FDF_SWEEP_STEP(4)
+        FDF_SWEEP_STEP(5)
+        FDF_SWEEP_STEP(6)
+        FDF_SWEEP_STEP(7)
+    }
+#undef FDF_SWEEP_STEP
+    // the last block ends on an odd step: at most its last row is still queued, and the
+    // ring still holds the rows it needs (and the score rows, which stop at p1 - 1)
+    sweep_drain<NMS, N, ScoreT>(sh, u, lk);
+    if constexpr (NMS != kNmsOff) sweep_finalize<ScoreT>(sh, u, p1 - 2, first_unfinal);
+}
+
+template <int NMS, int N>
+__global__ __launch_bounds__(kThreads) void fast_sweep_kernel(BandParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, score_bytes_for(NMS));
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63;
+    const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
+
+    // XCD-aware static task mapping (see fast_band_kernel)
+    const uint32_t b = blockIdx.x;
+    const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
+    const uint32_t task = k8 * q8 + min(k8, r8) + (b >> 3);
+    const uint32_t frame = task / P.bands_per_frame;
+    const uint32_t band = task - frame * P.bands_per_frame;
+    const uint32_t y0 = 3 + band * P.rows;
+    const uint32_t rows = min(P.rows, H - 3 - y0);
+
+    uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap);
+    uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap + align16(P.rows * nw * 4));
+    if (P.threshold >= 255) {                                        // no pixel can pass
+        if (tid == 0) P.counts[task] = 0;
+        return;
+    }
+    for (uint32_t i = tid; i < rows * nw; i += kThreads) bitmap[i] = 0;
+    __syncthreads();
+
+    uint8_t* wbase = smem_raw + wave * L.wave_bytes;
+    SweepShared sh;
+    sh.data = wbase + L.data;
+    sh.pq = reinterpret_cast<uint32_t*>(wbase + L.pq);
+    sh.ring = wbase + L.ring;
+    sh.kp = reinterpret_cast<uint32_t*>(wbase + L.kp);
+    sh.bitmap = bitmap;
+
+    UnitCtx u;
+    const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
+    u.src.W = W;
+    u.src.H = H;
+    u.src.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(img), 0,
+                                                 (int)(W * H + 15), 0x00020000);
+    u.t = P.threshold;
+    u.nw = nw;
+    u.y0 = (int)y0;
+    u.lane = lane;
+    u.flags = P.flags;
+    const LerpConsts lk = lerp_consts(P.threshold);
+
+    const uint32_t nunits = P.nstrips * P.nsub;
+    const uint32_t sub_rows = (rows + P.nsub - 1) / P.nsub;
+    if (!(P.flags & kFlagNoPrefilter)) {
+        for (uint32_t unit = wave; unit < nunits; unit += kWaves) {
+            const uint32_t strip = unit % P.nstrips, sub = unit / P.nstrips;
+            u.S = (int)(strip * kStripCols);
+            u.r0 = (int)(y0 + sub * sub_rows);
+            u.r1 = (int)min(y0 + (sub + 1) * sub_rows, y0 + rows);
+            if (u.r0 >= u.r1) continue;
+            sweep_unit<NMS, N>(sh, u, lk);
+        }
+    }
+    __syncthreads();
+
+    // ---- count keep-bits and write the band slot (as fast_band_kernel)
+    const uint32_t nwords = rows * nw;
+    const uint32_t per = (nwords + kThreads - 1) / kThreads;
+    const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);
+    uint32_t mine = 0;
+    for (uint32_t w = w_lo; w < w_hi; ++w) mine += __popc(bitmap[w]);
+    uint32_t incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += o;
+    }
+    if (lane == 63) wave_sum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const uint32_t v = wave_sum[w];
+        before += (uint32_t)w < wave ? v : 0u;
+        total += v;
+    }
+    if (tid == 0) P.counts[task] = total;
+    if (P.flags & kFlagNoEmit) return;
+    uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
+    if (total <= P.slot_bytes / 8) {
+        uint2* pts = reinterpret_cast<uint2*>(slot);
+        uint32_t idx = before + incl - mine;
+        for (uint32_t w = w_lo; w < w_hi; ++w) {
+            uint32_t bits = bitmap[w];
+            const uint32_t r = w / nw;
+            const uint32_t xb = (w - r * nw) * 32;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                pts[idx++] = make_uint2(xb + bit, y0 + r);
+            }
+        }
+    } else {
+        uint32_t* words = reinterpret_cast<uint32_t*>(slot);
+        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = bitmap[w];
+    }
+}
+
+typedef void (*SweepKernelFn)(BandParams);
+
+template <int NMS>
+static SweepKernelFn pick_sweep_n(uint32_t n) {
+    switch (n) {
+        case 9: return fast_sweep_kernel<NMS, 9>;
+        case 10: return fast_sweep_kernel<NMS, 10>;
+        case 11: return fast_sweep_kernel<NMS, 11>;
+        case 12: return fast_sweep_kernel<NMS, 12>;
+        case 13: return fast_sweep_kernel<NMS, 13>;
+        case 14: return fast_sweep_kernel<NMS, 14>;
+        case 15: return fast_sweep_kernel<NMS, 15>;
+        case 16: return fast_sweep_kernel<NMS, 16>;
+        default: return nullptr;
+    }
+}
+
+hipError_t launch_sweep(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
+                        hipStream_t stream) {
+    SweepKernelFn fn = nullptr;
+    switch (nms) {
+        case kNmsOff: fn = pick_sweep_n<kNmsOff>(n); break;
+        case kNmsMaxThreshold: fn = pick_sweep_n<kNmsMaxThreshold>(n); break;
+        case kNmsSumAbsolute: fn = pick_sweep_n<kNmsSumAbsolute>(n); break;
+        default: break;
+    }
+    if (!fn) return hipErrorInvalidValue;
+    const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, score_bytes_for(nms));
+    if (L.total > kSweepMaxLds) return hipErrorInvalidValue;
+    if (L.total > kMaxLds) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)L.total);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_compact(c, stream);
+}
+
+}  // namespace fdfk

@@ -210,3 +210,61 @@ def test_s2_1080p_counts():
     assert len(oracle.detect(img, 16, 9, 0)) == 30877
     assert len(oracle.detect(img, 16, 9, 1)) == 5426
     assert len(oracle.detect(img, 16, 12, 0)) == 0
+
+
+def _lane_segment_test(c, ring, t, n):
+    """numpy restatement of fdf_common.h lane_segment_test: bytes packed 4 per word (byte j
+    of word m = pixel 4j + m), lerp SWAR compares, flags gathered into the doubled circle
+    mask with the kernel's shift / fold / byte-permute, then the doubling-AND run test."""
+    ob, od = t & 1, (t + 1) & 1
+    kb = 128 - ((t + ob) >> 1)
+    kd = 255 - ((254 - t + od) >> 1)
+    ring = np.asarray(ring)
+
+    def word_flags(r, k):
+        fl = [0, 0, 0, 0]
+        for m in range(4):
+            for j in range(4):
+                v = _lerp(_lerp(np.array(ring[4 * j + m]), np.array(255 - c), r), np.array(k), 0)
+                fl[m] |= (int(v) & 0x80) << (8 * j)
+        return fl
+
+    def gather(f):
+        x = (((f[0] >> 7) & 0x01010101) | ((f[1] >> 6) & 0x02020202) |
+             ((f[2] >> 5) & 0x04040404) | ((f[3] >> 4) & 0x08080808))
+        x |= x >> 4
+        b0, b2 = x & 0xff, (x >> 16) & 0xff
+        return b0 | (b2 << 8) | (b0 << 16) | (b2 << 24)
+
+    def run(m):
+        m &= m >> 1
+        m &= m >> 2
+        m &= m >> 4
+        if n > 8:
+            m &= m >> (n - 8)
+        return (m & 0xffff) != 0
+
+    bright = run(gather(word_flags(ob, kb)))
+    dark = run(~gather(word_flags(od, kd)) & 0xffffffff)
+    return bright, dark
+
+
+def test_lane_segment_test_matches_oracle():
+    """The sweep kernel's per-lane segment test equals the reference's run test."""
+    rng = np.random.default_rng(5)
+    for k in range(4000):
+        c = int(rng.integers(0, 256))
+        t = int(rng.integers(0, 255))
+        n = int(rng.integers(9, 17))
+        if k % 2:   # bias towards corners: a long arc of one polarity
+            ring = rng.integers(0, 256, 16)
+            s0, ln = int(rng.integers(0, 16)), int(rng.integers(n - 1, 17))
+            hi = rng.integers(min(c + t + 1, 255), 256, ln) if rng.integers(2) else rng.integers(0, max(c - t, 1), ln)
+            for q in range(ln):
+                ring[(s0 + q) % 16] = hi[q]
+        else:
+            ring = rng.integers(0, 256, 16)
+        b, d = _lane_segment_test(c, ring.tolist(), t, n)
+        bright = [p > c + t for p in ring]
+        dark = [p < c - t for p in ring]
+        assert b == _consecutive(bright, n) and d == _consecutive(dark, n), (c, t, n, ring)

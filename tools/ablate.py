@@ -33,12 +33,18 @@ def main():
     out = torch.empty((args.frames * 50_000, 2), dtype=torch.int32, device="cuda")
     offs = torch.zeros(args.frames + 1, dtype=torch.int64, device="cuda")
     modes = {"off": 0, "maxt": 1, "sad": 2}
-    variants = [(v.split(":")[0], int(v.split(":")[1])) for v in args.variants.split(",")]
+    # mode:flags[:lds_budget] -- the budget (bytes per workgroup) overrides the geometry pick
+    variants = [tuple(v.split(":")) for v in args.variants.split(",")]
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream()
     for r in range(args.rounds):
-        for (mode, flags) in variants:
-            os.environ["FDF_DEBUG_FLAGS"] = str(flags)
+        for v in variants:
+            mode, flags = v[0], v[1]
+            os.environ["FDF_DEBUG_FLAGS"] = str(int(flags, 0))
+            if len(v) > 2:
+                os.environ["FDF_LDS_BUDGET"] = v[2]
+            else:
+                os.environ.pop("FDF_LDS_BUDGET", None)
             cfg = Config(16, 9, NonMaximalSuppression(modes[mode]))
             fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
             s = torch.cuda.Event(enable_timing=True)
@@ -48,13 +54,13 @@ def main():
                 fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
             e.record(stream)
             torch.cuda.synchronize()
-            times[(mode, flags)].append(s.elapsed_time(e) / args.iters)
+            times[v].append(s.elapsed_time(e) / args.iters)
     os.environ.pop("FDF_DEBUG_FLAGS", None)
     px = args.frames * args.width * args.height
     res = {}
-    for (mode, flags), ts in times.items():
+    for v, ts in times.items():
         med = float(np.median(ts))
-        res[f"{mode}:flags{flags}"] = {"ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+        res[":".join(v)] = {"ms_median": round(med, 4), "ms_min": round(min(ts), 4),
                                        "Gpix_s": round(px / med / 1e6, 1)}
     print(json.dumps(res, indent=1))
 
