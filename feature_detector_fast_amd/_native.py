@@ -24,8 +24,9 @@ FDF_ERR_ALLOC = 7
 # Every symbol include/fdf.h declares (tests/test_abi.py checks the .so exports them all).
 EXPORTED_SYMBOLS = (
     "fdf_abi_version", "fdf_status_string", "fdf_device_count", "fdf_validate",
-    "fdf_ctx_create", "fdf_ctx_destroy", "fdf_ctx_stream", "fdf_detect", "fdf_detect_batch",
-    "fdf_detect_device", "fdf_score_points",
+    "fdf_ctx_create", "fdf_ctx_destroy", "fdf_ctx_stream", "fdf_ctx_set_timing",
+    "fdf_ctx_timing", "fdf_detect", "fdf_detect_batch", "fdf_detect_device",
+    "fdf_score_points",
 )
 
 
@@ -94,6 +95,11 @@ def load():
     lib.fdf_ctx_destroy.argtypes = [vp]
     lib.fdf_ctx_stream.restype = vp
     lib.fdf_ctx_stream.argtypes = [vp]
+    lib.fdf_ctx_set_timing.restype = ctypes.c_int
+    lib.fdf_ctx_set_timing.argtypes = [vp, ctypes.c_int]
+    lib.fdf_ctx_timing.restype = ctypes.c_int
+    lib.fdf_ctx_timing.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float),
+                                   ctypes.POINTER(ctypes.c_float)]
     lib.fdf_detect.restype = ctypes.c_int
     lib.fdf_detect.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, ctypes.POINTER(sz)]
     lib.fdf_detect_batch.restype = ctypes.c_int
@@ -131,6 +137,17 @@ class Context:
     @property
     def stream(self):
         return self._lib.fdf_ctx_stream(self.handle)
+
+    def set_timing(self, enable=True):
+        """Record HIP events around the detector and compaction launches of each call."""
+        check(self._lib.fdf_ctx_set_timing(self.handle, 1 if enable else 0))
+
+    def timing(self):
+        """(calls, detector_ms_total, compaction_ms_total) since timing was enabled."""
+        n, a, b = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_float()
+        check(self._lib.fdf_ctx_timing(self.handle, ctypes.byref(n), ctypes.byref(a),
+                                       ctypes.byref(b)))
+        return n.value, a.value, b.value
 
     def close(self):
         if self.handle:

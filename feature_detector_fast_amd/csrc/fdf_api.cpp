@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 #include <new>
 
 #include "../../include/fdf.h"
@@ -29,7 +30,13 @@ struct fdf_ctx {
     unsigned long long* d_state = nullptr; size_t state_n = 0;     // compaction look-back
     uint32_t* d_ticket = nullptr;
     uint32_t epoch = 0;
+    // optional per-kernel timing (fdf_ctx_set_timing): 3 events around each call's launches
+    bool timing = false;
+    size_t timed = 0;                     // calls recorded since timing was enabled
+    std::vector<hipEvent_t> ev;           // 3 per recorded call, kMaxTimedCalls at most
 };
+
+constexpr size_t kMaxTimedCalls = 4096;
 
 namespace {
 
@@ -83,17 +90,19 @@ struct Geometry {
     uint32_t R, nstrips, nsub;
 };
 
-uint32_t gcd(uint32_t a, uint32_t b) { return b ? gcd(b, a % b) : a; }
 
 Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score_bytes) {
     Geometry g;
     g.nstrips = (w - 3 + fdfk::kStripCols - 1) / fdfk::kStripCols;
-    g.nsub = 4 / gcd(g.nstrips, 4);                    // units a multiple of the 4 waves
+    // >= 8 units per band, handed out dynamically to the 4 waves (measured: 2 per wave
+    // balances the workgroup better than 1, at a small cost in halo rows)
+    g.nsub = (8 + g.nstrips - 1) / g.nstrips;
+    if (const char* e = std::getenv("FDF_NSUB")) g.nsub = (uint32_t)std::strtoul(e, nullptr, 0);
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
-    // LDS per workgroup sets the workgroups per CU: 3 without NMS, 2 for max-threshold,
-    // SAD's 16-bit score ring leaves room for 1.
-    uint32_t budget = score_bytes == 0 ? 53 * 1024 : (score_bytes == 1 ? 80 * 1024 : fdfk::kSweepMaxLds);
+    // LDS per workgroup sets the workgroups per CU: 4 without NMS, 2 for max-threshold,
+    // SAD's 16-bit score ring leaves room for 1 (tools/ablate.py sweeps).
+    uint32_t budget = score_bytes == 0 ? 40000 : (score_bytes == 1 ? 80 * 1024 : fdfk::kSweepMaxLds);
     if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the
@@ -130,7 +139,8 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     const uint64_t ntasks = (uint64_t)bands * n_frames;
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
     const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw);
-    const uint64_t ngroups = (ntasks + fdfk::kCompactTasks - 1) / fdfk::kCompactTasks;
+    const uint32_t tpg = fdfk::compact_tasks_per_group((uint32_t)ntasks);
+    const uint64_t ngroups = (ntasks + tpg - 1) / tpg;
     int rc;
     if ((rc = ensure(&ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), false, stream))) return rc;
     if ((rc = ensure(&ctx->d_counts, &ctx->counts_n, (size_t)ntasks, false, stream))) return rc;
@@ -172,6 +182,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.ntasks = (uint32_t)ntasks;
     c.words_per_row = nw;
     c.slot_bytes = slot_bytes;
+    c.tasks_per_group = tpg;
     c.epoch = ctx->epoch;
     c.slots = ctx->d_slots;
     c.counts = ctx->d_counts;
@@ -180,8 +191,23 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.frame_offsets = d_offsets;
     c.state = ctx->d_state;
     c.ticket = ctx->d_ticket;
-    if (fdfk::launch_sweep(p, c, cfg->nms, cfg->count, stream) != hipSuccess)
-        return FDF_ERR_DEVICE;
+    hipEvent_t* ev = nullptr;
+    if (ctx->timing && ctx->timed < kMaxTimedCalls) {
+        while (ctx->ev.size() < 3 * (ctx->timed + 1)) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return FDF_ERR_DEVICE;
+            ctx->ev.push_back(e);
+        }
+        ev = &ctx->ev[3 * ctx->timed];
+    }
+    if (ev && hipEventRecord(ev[0], stream) != hipSuccess) return FDF_ERR_DEVICE;
+    if (fdfk::launch_sweep(p, cfg->nms, cfg->count, stream) != hipSuccess) return FDF_ERR_DEVICE;
+    if (ev && hipEventRecord(ev[1], stream) != hipSuccess) return FDF_ERR_DEVICE;
+    if (fdfk::launch_compact(c, stream) != hipSuccess) return FDF_ERR_DEVICE;
+    if (ev) {
+        if (hipEventRecord(ev[2], stream) != hipSuccess) return FDF_ERR_DEVICE;
+        ++ctx->timed;
+    }
     return FDF_OK;
 }
 
@@ -305,12 +331,40 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_state);
         (void)hipFree(ctx->d_ticket);
+        for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;
 }
 
 void* fdf_ctx_stream(fdf_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int fdf_ctx_set_timing(fdf_ctx* ctx, int enable) {
+    if (!ctx) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->timing = enable != 0;
+    ctx->timed = 0;
+    return FDF_OK;
+}
+
+int fdf_ctx_timing(fdf_ctx* ctx, uint32_t* calls, float* detect_ms, float* compact_ms) {
+    if (!ctx || !calls || !detect_ms || !compact_ms) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    *calls = (uint32_t)ctx->timed;
+    *detect_ms = *compact_ms = 0.0f;
+    for (size_t k = 0; k < ctx->timed; ++k) {
+        const hipEvent_t* e = &ctx->ev[3 * k];
+        float a = 0.0f, b = 0.0f;
+        if (hipEventSynchronize(e[2]) != hipSuccess ||
+            hipEventElapsedTime(&a, e[0], e[1]) != hipSuccess ||
+            hipEventElapsedTime(&b, e[1], e[2]) != hipSuccess)
+            return FDF_ERR_DEVICE;
+        *detect_ms += a;
+        *compact_ms += b;
+    }
+    return FDF_OK;
+}
 
 int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
                size_t stride_bytes, const fdf_config* cfg, fdf_point* out, size_t cap,

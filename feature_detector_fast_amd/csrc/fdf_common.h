@@ -1,5 +1,5 @@
-// fdf_common.h -- device helpers shared by the FAST kernels (fdf_kernels.hip, fdf_sweep.hip):
-// circle geometry, byte-SWAR comparisons, wave ballots, the bit-sliced arc test and the
+// fdf_common.h -- device helpers of the FAST kernels (fdf_sweep.hip, fdf_kernels.hip):
+// circle geometry, byte-SWAR comparisons, wave ballots, the per-lane segment test and the
 // two NMS score functions of the reference (iwanders/feature_detector_fast).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -50,26 +50,10 @@ __device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
     return k;
 }
 
-// Cyclic run test on bit-sliced masks: bit k of b[i] = "lane k's circle pixel i qualifies".
-// Returns the lanes whose ring holds a run of >= N qualifying pixels (src/fast_simd.rs:247-295).
-template <int N>
-__device__ __forceinline__ uint64_t arc_test(const uint64_t (&b)[16]) {
-    uint64_t p2[16], p4[16], p8[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p2[i] = b[i] & b[(i + 1) & 15];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p4[i] = p2[i] & p2[(i + 2) & 15];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p8[i] = p4[i] & p4[(i + 4) & 15];
-    uint64_t any = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) any |= p8[i] & p8[(i + N - 8) & 15];
-    return any;
-}
-
-// Per-lane form of the segment test (each lane tests its own pixel, all in VALU).
+// Segment test, one pixel per lane, all in VALU.
 // run_of: `m` holds the 16 circle flags twice (pixel i at bits i and i+16); true when some
-// cyclic run of >= N flags is set (src/fast_simd.rs:247-295).  Doubling ANDs as arc_test.
+// cyclic run of >= N flags is set (src/fast_simd.rs:247-295), by doubling ANDs: after the
+// k-th AND, bit i means "flags i .. i + 2^k - 1 are all set".
 template <int N>
 __device__ __forceinline__ bool run_of(uint32_t m) {
     m &= m >> 1;

@@ -1,5 +1,5 @@
-// fdf_kernels.h -- shared between the HIP kernels (fdf_kernels.hip) and the C-ABI host
-// layer (fdf_api.cpp): tiling constants, LDS layout and launch parameters.
+// fdf_kernels.h -- shared between the HIP kernels (fdf_sweep.hip, fdf_kernels.hip) and the
+// C-ABI host layer (fdf_api.cpp): geometry constants, LDS layout and launch parameters.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -12,13 +12,6 @@ constexpr int kNmsSumAbsolute = 2;
 
 constexpr int kThreads = 256;                 // 4 waves of 64 lanes
 constexpr int kWaves = kThreads / 64;
-constexpr int kChunk = 1024;                  // centre columns per chunk (256 lanes x 4 px)
-constexpr int kGroups = kChunk / 4 + 2;       // 4-pixel groups incl. a 1-group ring each side
-constexpr int kPitch = kChunk + 32;           // input tile row pitch in bytes (16-B aligned)
-constexpr int kScorePitch = kChunk + 16;      // score row pitch in elements (group gi at 4*gi)
-constexpr int kGroupQ = 80;                   // per-wave queue of candidate groups (15 + 64)
-constexpr int kPixelQ = 128;                  // per-wave queue of candidate pixels (63 + 64)
-constexpr int kKpCap = 1024;                  // per-chunk NMS keypoint list
 constexpr uint32_t kMaxLds = 64 * 1024;       // default dynamic-LDS limit per workgroup
 constexpr int kCompactTasks = 256;            // tasks per workgroup of the compaction kernel
 
@@ -26,9 +19,8 @@ constexpr int kCompactTasks = 256;            // tasks per workgroup of the comp
 // variable by the host layer; never part of the C ABI.  Results are wrong when set.
 constexpr uint32_t kFlagNoFullTest = 1;   // candidates are never tested (no keypoints)
 constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (counts only)
-constexpr uint32_t kFlagNoPrefilter = 4;  // skip the per-group pre-filter loop (sweep: units)
-constexpr uint32_t kFlagNoLoad = 8;       // band kernel: skip the tile loads; sweep: rows are
-                                          // streamed and compared but never pre-filtered
+constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compaction only)
+constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
 
 // Column-sweep kernel (fdf_sweep.hip): per-wave LDS region + the band bitmap.
 constexpr int kStripCols = 992;               // centres per wave strip (62 lanes x 16 columns)
@@ -65,29 +57,7 @@ __host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t score_by
     return (rows + 3 + (score_bytes ? 2 : 0) + 7) & ~7u;
 }
 
-struct LdsLayout {
-    uint32_t tile, scores, bitmap, gq_item, gq_cand, pq, kp_list, misc, total;
-};
-
 __host__ __device__ inline uint32_t align16(uint32_t v) { return (v + 15u) & ~15u; }
-
-
-// R = centre rows per band, nw = bitmap words per image row, score_bytes = 0 (no NMS),
-// 1 (max-threshold scores fit u8) or 2 (sum-of-absolute-differences scores need u16).
-__host__ __device__ inline LdsLayout make_layout(uint32_t R, uint32_t nw, uint32_t score_bytes) {
-    LdsLayout L;
-    uint32_t o = 0;
-    L.tile = o;    o += align16((R + 8) * kPitch);
-    L.scores = o;  o += align16((R + 2) * kScorePitch * score_bytes);
-    L.bitmap = o;  o += align16(R * nw * 4);
-    L.gq_item = o; o += align16(kWaves * kGroupQ * 4);
-    L.gq_cand = o; o += align16(kWaves * kGroupQ * 4);
-    L.pq = o;      o += align16(kWaves * kPixelQ * 4);
-    L.kp_list = o; o += score_bytes ? align16(kKpCap * 4) : 0;
-    L.misc = o;    o += 64;
-    L.total = o;
-    return L;
-}
 
 __host__ __device__ inline uint32_t score_bytes_for(uint32_t nms) {
     return nms == kNmsOff ? 0u : (nms == kNmsMaxThreshold ? 1u : 2u);
@@ -115,23 +85,27 @@ struct BandParams {
     uint32_t nstrips, nsub;      // sweep kernel: column strips x sub-bands per band
 };
 
+// Bands per compaction workgroup: enough groups (~1024) to spread the copy over the chip.
+__host__ __device__ inline uint32_t compact_tasks_per_group(uint32_t ntasks) {
+    const uint32_t t = ntasks / 1024;
+    return t < 1 ? 1u : (t > (uint32_t)kCompactTasks ? (uint32_t)kCompactTasks : t);
+}
+
 struct CompactParams {
     uint32_t width, height, rows, bands_per_frame, ntasks, words_per_row, slot_bytes;
+    uint32_t tasks_per_group;        // compact_tasks_per_group(ntasks)
     uint32_t epoch;                  // look-back generation tag, 1..65535
     const uint8_t* slots;
     const uint32_t* counts;
     uint2* out;
     uint64_t cap;
     uint64_t* frame_offsets;         // frames + 1 entries
-    unsigned long long* state;       // >= ceil(ntasks / kCompactTasks) look-back words
+    unsigned long long* state;       // >= ceil(ntasks / tasks_per_group) look-back words
     uint32_t* ticket;                // zero between launches (self-resetting)
 };
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);
-hipError_t launch_sweep(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
-                        hipStream_t stream);
-hipError_t launch_detect(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
-                         hipStream_t stream);
+hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
 hipError_t launch_score_points(const uint8_t* img, uint32_t width, const uint2* pts,
                                uint32_t npts, uint32_t nms, uint32_t t, uint32_t n,
                                uint16_t* out, hipStream_t stream);

@@ -48,22 +48,37 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
 }
 
 struct RowSource {
-    __amdgpu_buffer_rsrc_t rs;   // the frame; num_records = W * H + 15 (reads beyond return 0)
+    __amdgpu_buffer_rsrc_t rs;   // the frame; num_records = W * H + 15, or W * H when EXACT
     uint32_t W, H;
+    int tail_row;                // EXACT: rows >= tail_row may have windows crossing W * H
 };
 
 constexpr int kOutOfRange = 0x7ffffff0;   // a buffer offset past any frame: loads return 0
 
 // Bytes [xb, xb+16) of image row y: one 16-byte buffer load at any byte offset (gfx950
-// buffer loads need no alignment).  Branch-free, so the compiler's vmcnt bookkeeping keeps
-// the row prefetch in flight; rows outside the frame and negative offsets read 0.  Columns
-// outside [0, W) hold the neighbouring row's bytes -- only halo lanes and non-centre pixels
-// see them.
+// buffer loads need no alignment).  No branch, so the row prefetch stays a plain stream the
+// compiler's vmcnt bookkeeping can count.  Rows outside the frame and negative offsets read
+// 0; columns outside [0, W) hold neighbouring bytes (the next row, or up to 15 bytes past
+// the frame, which belong to the next frame of the batch or its stride gap) -- only halo
+// lanes and non-centre pixels see them.  EXACT (the last frame of a batch, whose end may be
+// the end of the caller's allocation): the rows whose windows can cross W * H are read byte
+// by byte against num_records = W * H, so nothing past the frame is touched.
+template <bool EXACT>
 __device__ __forceinline__ u32x4 load_row(const RowSource& src, int y, int xb) {
     const int off = y * (int)src.W + xb;
     const bool in = y >= 0 && y < (int)src.H && off >= 0;
-    return __builtin_bit_cast(
-        u32x4, __builtin_amdgcn_raw_buffer_load_b128(src.rs, in ? off : kOutOfRange, 0, 0));
+    const int o = in ? off : kOutOfRange;
+    if constexpr (EXACT) {
+        if (y >= src.tail_row) {   // wave-uniform
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                w[k >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(src.rs, o + k, 0, 0)
+                             << (8 * (k & 3));
+            return u32x4{w[0], w[1], w[2], w[3]};
+        }
+    }
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(src.rs, o, 0, 0));
 }
 
 struct SweepShared {
@@ -213,7 +228,7 @@ __device__ __forceinline__ RowFlags compare_rows(const u32x4& x, const u32x4& nc
     return f;
 }
 
-template <int NMS, int N>
+template <int NMS, int N, bool EXACT>
 __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     using ScoreT = typename std::conditional<NMS == kNmsSumAbsolute, uint16_t, uint8_t>::type;
     const uint32_t lane = u.lane;
@@ -250,9 +265,9 @@ __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& 
     u32x4 C[4];                                        // rows yv..yv+3, slot (row - ys) & 3
     u32x4 Q[kSweepPrefetch];                           // row ys+k+3 (+8m) in slot (k+3) & 7
 #pragma unroll
-    for (int k = 0; k < 3; ++k) C[k] = load_row(u.src, ys + k, xb);
+    for (int k = 0; k < 3; ++k) C[k] = load_row<EXACT>(u.src, ys + k, xb);
 #pragma unroll
-    for (int k = 0; k < kSweepPrefetch; ++k) Q[(k + 3) & 7] = load_row(u.src, ys + 3 + k, xb);
+    for (int k = 0; k < kSweepPrefetch; ++k) Q[(k + 3) & 7] = load_row<EXACT>(u.src, ys + 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < 3; ++k) ring[k * 64] = C[k];
     RowFlags V[4];                                     // vertical flags, slot (row-ys) & 3
@@ -263,7 +278,7 @@ __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& 
         const int yv = ys + i;                                                               \
         const u32x4 s = Q[((J) + 3) & 7];                  /* row yv + 3 */                  \
         ring[(((J) + 3) & 7) * 64] = s;                                                      \
-        Q[((J) + 3) & 7] = load_row(u.src, yv + 3 + kSweepPrefetch, xb);                     \
+        Q[((J) + 3) & 7] = load_row<EXACT>(u.src, yv + 3 + kSweepPrefetch, xb);                     \
         C[((J) + 3) & 3] = s;                                                                \
         const u32x4 c = C[(J) & 3];                                                          \
         const u32x4 nc = ~c;                                                                 \
@@ -377,7 +392,9 @@ __global__ __launch_bounds__(kThreads) void fast_sweep_kernel(BandParams P) {
         if (tid == 0) P.counts[task] = 0;
         return;
     }
+    uint32_t* unit_ctr = wave_sum + kWaves;
     for (uint32_t i = tid; i < rows * nw; i += kThreads) bitmap[i] = 0;
+    if (tid == 0) *unit_ctr = 0;
     __syncthreads();
 
     uint8_t* wbase = smem_raw + wave * L.wave_bytes;
@@ -392,8 +409,11 @@ __global__ __launch_bounds__(kThreads) void fast_sweep_kernel(BandParams P) {
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
     u.src.W = W;
     u.src.H = H;
-    u.src.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(img), 0,
-                                                 (int)(W * H + 15), 0x00020000);
+    const bool last_frame = frame + 1 == P.ntasks / P.bands_per_frame;
+    const __amdgpu_buffer_rsrc_t rs_pad = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(img), 0, (int)(W * H + 15), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_exact = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(img), 0, (int)(W * H), 0x00020000);
     u.t = P.threshold;
     u.nw = nw;
     u.y0 = (int)y0;
@@ -403,14 +423,35 @@ __global__ __launch_bounds__(kThreads) void fast_sweep_kernel(BandParams P) {
 
     const uint32_t nunits = P.nstrips * P.nsub;
     const uint32_t sub_rows = (rows + P.nsub - 1) / P.nsub;
+    // units are handed out dynamically: a wave that finishes early takes the next one
+    // instead of idling at the workgroup barrier
     if (!(P.flags & kFlagNoPrefilter)) {
-        for (uint32_t unit = wave; unit < nunits; unit += kWaves) {
+        for (;;) {
+            uint32_t unit = 0;
+            if (lane == 0) unit = atomicAdd(unit_ctr, 1u);
+            unit = __builtin_amdgcn_readfirstlane(unit);
+            if (unit >= nunits) break;
             const uint32_t strip = unit % P.nstrips, sub = unit / P.nstrips;
             u.S = (int)(strip * kStripCols);
+            {   // first row whose last lane's window can end past W * H
+                const int last_end = u.S - 16 + 16 * 63 + 16;
+                const int num = (int)(W * H) - last_end;
+                u.src.tail_row = num < 0 ? 0 : num / (int)W + 1;
+            }
             u.r0 = (int)(y0 + sub * sub_rows);
             u.r1 = (int)min(y0 + (sub + 1) * sub_rows, y0 + rows);
             if (u.r0 >= u.r1) continue;
-            sweep_unit<NMS, N>(sh, u, lk);
+            // rows the sweep loads: up to r1 + ringr + 3 rounded to the 8-step block + 8 ahead
+            const int ringr = NMS == kNmsOff ? 0 : 1;
+            const int ys = u.r0 - ringr - 3;
+            const int steps = (u.r1 + ringr - ys + 7) & ~7;
+            if (last_frame && ys + steps + 2 + kSweepPrefetch >= u.src.tail_row) {
+                u.src.rs = rs_exact;
+                sweep_unit<NMS, N, true>(sh, u, lk);
+            } else {
+                u.src.rs = rs_pad;
+                sweep_unit<NMS, N, false>(sh, u, lk);
+            }
         }
     }
     __syncthreads();
@@ -475,8 +516,7 @@ static SweepKernelFn pick_sweep_n(uint32_t n) {
     }
 }
 
-hipError_t launch_sweep(const BandParams& p, const CompactParams& c, uint32_t nms, uint32_t n,
-                        hipStream_t stream) {
+hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream) {
     SweepKernelFn fn = nullptr;
     switch (nms) {
         case kNmsOff: fn = pick_sweep_n<kNmsOff>(n); break;
@@ -494,9 +534,7 @@ hipError_t launch_sweep(const BandParams& p, const CompactParams& c, uint32_t nm
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return launch_compact(c, stream);
+    return hipGetLastError();
 }
 
 }  // namespace fdfk

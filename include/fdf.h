@@ -84,6 +84,14 @@ void fdf_ctx_destroy(fdf_ctx* ctx);
 /* The context's hipStream_t (as void*), for callers that enqueue their own work beside it. */
 void* fdf_ctx_stream(fdf_ctx* ctx);
 
+/* Profiling (extension, no reference counterpart): while enabled, each detect call on the
+ * context (up to 4096 of them) records HIP events on its stream around its two kernel
+ * launches -- the detector (pre-filter, segment test, NMS, per-band slots) and the
+ * raster-order compaction.  fdf_ctx_timing waits for the recorded calls and returns their
+ * number and the summed durations of both launches in ms.  Enabling resets the record. */
+int fdf_ctx_set_timing(fdf_ctx* ctx, int enable);
+int fdf_ctx_timing(fdf_ctx* ctx, uint32_t* calls, float* detect_ms, float* compact_ms);
+
 /*
  * Replaces fast_simd::detector(img, config) -> Vec<Point> (src/fast_simd.rs:847).
  * Host image (row-major u8, `stride_bytes` >= width; GrayImage always has stride == width),
@@ -114,7 +122,8 @@ int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint3
  * and d_frame_offsets[n_frames] the total, even when the total exceeds `cap` (points with
  * index >= cap are not written).  Argument and shape errors are returned synchronously.
  * The context's workspace is reused by each call: calls on one context must be issued on
- * one stream (or otherwise serialised).
+ * one stream (or otherwise serialised).  Frames before the last may be read up to 15 bytes
+ * past their end (inside the batch allocation); the last frame is read exactly.
  */
 int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
                       uint32_t width, uint32_t height, uint64_t frame_stride_bytes,

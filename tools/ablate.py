@@ -33,7 +33,8 @@ def main():
     out = torch.empty((args.frames * 50_000, 2), dtype=torch.int32, device="cuda")
     offs = torch.zeros(args.frames + 1, dtype=torch.int64, device="cuda")
     modes = {"off": 0, "maxt": 1, "sad": 2}
-    # mode:flags[:lds_budget] -- the budget (bytes per workgroup) overrides the geometry pick
+    # mode:flags[:lds_budget[:nsub]] -- budget (bytes per workgroup) and sub-bands per band
+    # override the geometry pick (0 = default)
     variants = [tuple(v.split(":")) for v in args.variants.split(",")]
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream()
@@ -41,10 +42,11 @@ def main():
         for v in variants:
             mode, flags = v[0], v[1]
             os.environ["FDF_DEBUG_FLAGS"] = str(int(flags, 0))
-            if len(v) > 2:
-                os.environ["FDF_LDS_BUDGET"] = v[2]
-            else:
-                os.environ.pop("FDF_LDS_BUDGET", None)
+            for k, name in ((2, "FDF_LDS_BUDGET"), (3, "FDF_NSUB")):
+                if len(v) > k and v[k] != "0":
+                    os.environ[name] = v[k]
+                else:
+                    os.environ.pop(name, None)
             cfg = Config(16, 9, NonMaximalSuppression(modes[mode]))
             fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
             s = torch.cuda.Event(enable_timing=True)

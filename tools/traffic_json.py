@@ -1,0 +1,50 @@
+"""Per-launch HBM traffic of the detector kernel from two rocprofv3 --pmc passes.
+
+    python tools/traffic_json.py FETCH_DIR WRITE_DIR CFG_KEY OUT.json [--kernel fast_sweep]
+
+FETCH_SIZE and WRITE_SIZE (KiB, TCC memory-side requests; separate passes -- they do not fit
+one) are averaged over the kernel's dispatches.  gfx950 tallies a wide coalesced read at
+half its bytes (MI355X_MICROARCH.md, HBM/rocprofv3 section), so
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+The result is merged into OUT.json under CFG_KEY (bench.py reads it as roofline.traffic).
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import load  # noqa: E402
+
+
+def mean_counter(d, name, kernel):
+    per, _ = load(d, kernel)
+    vals = [c[name] for c in per.values() if name in c]
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    kernel = "fast_sweep"
+    if "--kernel" in sys.argv:
+        kernel = sys.argv[sys.argv.index("--kernel") + 1]
+        args = [a for a in args if a != kernel]
+    fdir, wdir, key, out = args[:4]
+    fetch, nf = mean_counter(fdir, "FETCH_SIZE", kernel)
+    write, nw = mean_counter(wdir, "WRITE_SIZE", kernel)
+    if fetch is None or write is None:
+        sys.exit("counters missing")
+    entry = {"kernel": kernel, "dispatches": [nf, nw], "FETCH_SIZE_KiB": fetch,
+             "WRITE_SIZE_KiB": write, "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
+             "correction": "gfx950: FETCH_SIZE x2 (half-tallied wide reads)"}
+    data = {}
+    if os.path.exists(out):
+        with open(out) as f:
+            data = json.load(f)
+    data[key] = entry
+    with open(out, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print(json.dumps({key: entry}))
+
+
+if __name__ == "__main__":
+    main()
