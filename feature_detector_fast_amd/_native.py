@@ -9,7 +9,9 @@ import os
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfdf.so")
+# FDF_LIB_PATH: another build of the same library (A/B timing of two kernel versions,
+# tools/build_rev.sh); the default is the in-tree build.
+LIB_PATH = os.environ.get("FDF_LIB_PATH") or os.path.join(_HERE, "libfdf.so")
 
 # include/fdf.h enum fdf_status
 FDF_OK = 0

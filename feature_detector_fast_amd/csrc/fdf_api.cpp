@@ -93,16 +93,19 @@ struct Geometry {
 
 Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score_bytes) {
     Geometry g;
-    g.nstrips = (w - 3 + fdfk::kStripCols - 1) / fdfk::kStripCols;
-    // >= 8 units per band, handed out dynamically to the 4 waves (measured: 2 per wave
-    // balances the workgroup better than 1, at a small cost in halo rows)
-    g.nsub = (8 + g.nstrips - 1) / g.nstrips;
+    const uint32_t lc = (uint32_t)fdfk::lane_cols_for(score_bytes ? 1u : 0u);
+    const uint32_t sc = (uint32_t)fdfk::strip_cols((int)lc);
+    g.nstrips = (w - 3 + sc - 1) / sc;
+    // >= 4 units per band (one per wave), handed out dynamically; taller units (fewer halo
+    // rows) measured faster than more, shorter units for balance
+    g.nsub = (4 + g.nstrips - 1) / g.nstrips;
     if (const char* e = std::getenv("FDF_NSUB")) g.nsub = (uint32_t)std::strtoul(e, nullptr, 0);
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
-    // LDS per workgroup sets the workgroups per CU: 4 without NMS, 2 for max-threshold,
-    // SAD's 16-bit score ring leaves room for 1 (tools/ablate.py sweeps).
-    uint32_t budget = score_bytes == 0 ? 40000 : (score_bytes == 1 ? 80 * 1024 : fdfk::kSweepMaxLds);
+    // LDS per workgroup sets the workgroups per CU: 3 for NMS off (taller bands beat a 4th
+    // workgroup), 4 for max-threshold, 3 for SAD's 16-bit score ring (DESIGN.md §4.1;
+    // tools/ablate.py sweeps).
+    uint32_t budget = score_bytes == 0 ? 48000 : (score_bytes == 2 ? 53000 : 40000);
     if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the
@@ -110,7 +113,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score
     double best = -1.0;
     g.R = 0;
     for (uint32_t R = g.nsub; R <= 256 && R < centre_rows + g.nsub; R += g.nsub) {
-        if (fdfk::make_sweep_layout(R, nw, score_bytes).total > budget) break;
+        if (fdfk::make_sweep_layout(R, nw, score_bytes, lc).total > budget) break;
         const uint64_t tasks = (uint64_t)n_frames * ((centre_rows + R - 1) / R);
         if (tasks < 1024) break;
         const uint32_t steps = fdfk::sweep_steps(R / g.nsub, score_bytes);
@@ -120,7 +123,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score
     if (g.R == 0) {
         const uint32_t unit = 8 - 3 - (score_bytes ? 2 : 0);
         g.R = g.nsub * unit;
-        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, score_bytes).total > budget)
+        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, score_bytes, lc).total > budget)
             g.R -= g.nsub;
     }
     return g;
@@ -134,7 +137,8 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     const Geometry geo = pick_geometry(n_frames, w, h, sb);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
-    if (fdfk::make_sweep_layout(R, nw, sb).total > fdfk::kSweepMaxLds) return FDF_ERR_SIZE;
+    if (fdfk::make_sweep_layout(R, nw, sb, fdfk::lane_cols_for(cfg->nms)).total > fdfk::kSweepMaxLds)
+        return FDF_ERR_SIZE;
     const uint32_t bands = (h - 6 + R - 1) / R;
     const uint64_t ntasks = (uint64_t)bands * n_frames;
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;

@@ -23,7 +23,10 @@ constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compa
 constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
 
 // Column-sweep kernel (fdf_sweep.hip): per-wave LDS region + the band bitmap.
-constexpr int kStripCols = 992;               // centres per wave strip (62 lanes x 16 columns)
+// Columns per lane: 16 without NMS; 8 with NMS, whose per-wave score ring and keypoint list
+// would otherwise halve the waves per CU.  A strip is 62 lanes wide (lanes 0, 63: halo).
+__host__ __device__ constexpr int lane_cols_for(uint32_t nms) { return nms == 0 ? 16 : 8; }
+__host__ __device__ constexpr int strip_cols(int lc) { return 62 * lc; }
 constexpr int kSweepRing = 4;                 // NMS score ring rows per wave (power of two)
 constexpr int kSweepDataRows = 8;             // pixel-row ring per wave read by the full test
 constexpr int kSweepPrefetch = 8;             // rows loaded ahead of the sweep (register queue)
@@ -38,12 +41,12 @@ struct SweepLayout {
 __host__ __device__ inline uint32_t align16(uint32_t v);
 
 __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw,
-                                                         uint32_t score_bytes) {
+                                                         uint32_t score_bytes, uint32_t lc) {
     SweepLayout L;
     uint32_t o = 0;
-    L.data = o;     o += kSweepDataRows * 1024;
+    L.data = o;     o += kSweepDataRows * 64 * lc;
     L.pq = o;       o += kSweepPixelQ * 4;
-    L.ring = o;     o += kSweepRing * 1024 * score_bytes;
+    L.ring = o;     o += kSweepRing * 64 * lc * score_bytes;
     L.kp = o;       o += score_bytes ? kSweepKpCap * 4 : 0;
     L.wave_bytes = align16(o);
     L.bitmap = 4 * L.wave_bytes;

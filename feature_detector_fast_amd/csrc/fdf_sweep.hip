@@ -4,10 +4,12 @@
 // determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
 //
 // One workgroup (4 waves) owns a band of R full-width centre rows of one frame.  The band is
-// cut into units = (column strip of 992 centres) x (sub-band of rows); a wave sweeps a unit
-// top to bottom:
-//   * lane l owns 16 columns (one 16-B buffer load per row); lanes 0 and 63 are halo lanes
-//     that only feed their neighbours, so a strip covers 62 x 16 = 992 centres;
+// cut into units = (column strip) x (sub-band of rows); a wave sweeps a unit top to bottom
+// (DESIGN.md §4.1):
+//   * lane l owns LC columns (one LC-byte buffer load per row; LC = 16 without NMS, 8 with
+//     NMS, whose score ring and keypoint list would otherwise halve the waves per CU); lanes
+//     0 and 63 are halo lanes that only feed their neighbours, so a strip covers 62 x LC
+//     centres;
 //   * pixel rows stream through an 8-deep register queue (loads run 8 rows ahead, never
 //     guarded by a branch, so the prefetch stays in flight), then into a per-wave LDS ring of
 //     the last 8 rows that the full test reads;
@@ -16,7 +18,7 @@
 //     pair (I(x), I(x+3)) gives E-flags for x and W-flags for x+3 (a 3-byte shift, with the
 //     neighbouring lane's bytes via DPP).  Comparisons are byte-SWAR v_lerp_u8 (exact per
 //     byte, see fdf_common.h), so the cardinal pre-filter (src/fast_simd.rs:441-509) costs
-//     32 lerps per 16 pixels instead of 64;
+//     2 lerps per pixel instead of 4;
 //   * candidate pixels go straight into a per-wave queue (one per lane per round) and are
 //     tested 64 at a time, one pixel per lane, with the VALU segment test of fdf_common.h on
 //     bytes read from the LDS ring (no global loads outside the row stream); every 2 rows
@@ -37,6 +39,12 @@
 namespace fdfk {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// A lane's LC bytes of one pixel row (LC / 4 dwords).
+template <int LC> struct LaneRow;
+template <> struct LaneRow<16> { using type = u32x4; };
+template <> struct LaneRow<8> { using type = u32x2; };
 
 // DPP whole-wave shifts (GFX9 encodings): lane i reads lane i+1 / lane i-1; the lane that
 // falls off the wave reads 0 (it is a halo lane whose results are never used).
@@ -50,12 +58,13 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
 struct RowSource {
     __amdgpu_buffer_rsrc_t rs;   // the frame; num_records = W * H + 15, or W * H when EXACT
     uint32_t W, H;
+    int ylast;                   // last row the unit needs: later prefetches read nothing
     int tail_row;                // EXACT: rows >= tail_row may have windows crossing W * H
 };
 
 constexpr int kOutOfRange = 0x7ffffff0;   // a buffer offset past any frame: loads return 0
 
-// Bytes [xb, xb+16) of image row y: one 16-byte buffer load at any byte offset (gfx950
+// Bytes [xb, xb+LC) of image row y: one LC-byte buffer load at any byte offset (gfx950
 // buffer loads need no alignment).  No branch, so the row prefetch stays a plain stream the
 // compiler's vmcnt bookkeeping can count.  Rows outside the frame and negative offsets read
 // 0; columns outside [0, W) hold neighbouring bytes (the next row, or up to 15 bytes past
@@ -63,28 +72,33 @@ constexpr int kOutOfRange = 0x7ffffff0;   // a buffer offset past any frame: loa
 // lanes and non-centre pixels see them.  EXACT (the last frame of a batch, whose end may be
 // the end of the caller's allocation): the rows whose windows can cross W * H are read byte
 // by byte against num_records = W * H, so nothing past the frame is touched.
-template <bool EXACT>
-__device__ __forceinline__ u32x4 load_row(const RowSource& src, int y, int xb) {
+template <int LC, bool EXACT>
+__device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& src, int y,
+                                                              int xb) {
+    using RowV = typename LaneRow<LC>::type;
     const int off = y * (int)src.W + xb;
-    const bool in = y >= 0 && y < (int)src.H && off >= 0;
+    const bool in = y >= 0 && y < (int)src.H && y <= src.ylast && off >= 0;
     const int o = in ? off : kOutOfRange;
     if constexpr (EXACT) {
         if (y >= src.tail_row) {   // wave-uniform
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            RowV r = (RowV)(0u);
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                w[k >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(src.rs, o + k, 0, 0)
+            for (int k = 0; k < LC; ++k)
+                r[k >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(src.rs, o + k, 0, 0)
                              << (8 * (k & 3));
-            return u32x4{w[0], w[1], w[2], w[3]};
+            return r;
         }
     }
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(src.rs, o, 0, 0));
+    if constexpr (LC == 16)
+        return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b128(src.rs, o, 0, 0));
+    else
+        return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b64(src.rs, o, 0, 0));
 }
 
 struct SweepShared {
-    uint8_t* data;         // kSweepDataRows x 1024 pixel bytes, slot (row - ys) & 7
+    uint8_t* data;         // kSweepDataRows x 64*LC pixel bytes, slot (row - ys) & 7
     uint32_t* pq;          // kSweepPixelQ: (row << 10) | strip column
-    void* ring;            // kSweepRing x 1024 scores (NMS)
+    void* ring;            // kSweepRing x 64*LC scores (NMS)
     uint32_t* kp;          // kSweepKpCap: (row << 10) | strip column
     uint32_t* bitmap;      // band keep-bits, R x words_per_row
 };
@@ -102,68 +116,93 @@ struct UnitCtx {
     uint32_t flags;        // BandParams::flags (ablation runs only)
 };
 
-template <typename ScoreT>
+template <int LC, typename ScoreT>
 __device__ __forceinline__ ScoreT* ring_at(const SweepShared& sh, int y, int cl) {
-    return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kSweepRing - 1)) * 1024 + cl;
+    return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kSweepRing - 1)) * (64 * LC) + cl;
 }
 
-// Full test of `count` (<= 64) queued pixels from pq[0..count), one per lane (per-lane
-// VALU segment test, fdf_common.h).
-template <int NMS, int N, typename ScoreT>
-__device__ __forceinline__ void sweep_test(const SweepShared& sh, UnitCtx& u,
-                                           const LerpConsts& lk, const uint32_t* pq,
-                                           uint32_t count) {
-    const uint32_t lane = u.lane;
-    const bool act = lane < count;
-    const uint32_t code = act ? pq[lane] : 0u;
-    const int y = (int)(code >> 10), cl = (int)(code & 1023u);
-    const int x = u.S - 16 + cl;
+// Full test of up to 64 queued pixels, one per lane (per-lane VALU segment test,
+// fdf_common.h), in two halves so that the LDS reads of a batch can be in flight while the
+// sweep does other work: gather reads the pixel codes and their 17 bytes from the row ring,
+// evaluate tests them and records keypoints / scores.
+struct PendingTest {
+    uint32_t code;         // (row << 10) | strip column
+    bool act;
+    uint32_t c, p[16];
+};
+
+template <int LC>
+__device__ __forceinline__ PendingTest sweep_gather(const SweepShared& sh, const UnitCtx& u,
+                                                    const uint32_t* pq, uint32_t count) {
+    PendingTest t;
+    t.act = u.lane < count;
+    t.code = t.act ? pq[u.lane] : 0u;
+    const int y = (int)(t.code >> 10), cl = (int)(t.code & 1023u);
     // 7x7 neighbourhood from the LDS row ring: row y+dy in slot (y + dy - ys) & 7
     const int rel = y - u.ys;
-    const uint8_t* d = sh.data + (act ? cl : 16);
+    const uint8_t* d = sh.data + (t.act ? cl : LC);
     uint32_t base[7];
 #pragma unroll
-    for (int r = 0; r < 7; ++r) base[r] = (uint32_t)((rel + r - 3) & (kSweepDataRows - 1)) << 10;
-    uint32_t p[16];
+    for (int r = 0; r < 7; ++r)
+        base[r] = (uint32_t)((rel + r - 3) & (kSweepDataRows - 1)) * (64 * LC);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = d[base[circle_dy(i) + 3] + circle_dx(i)];
-    const uint32_t c = d[base[3]];
+    for (int i = 0; i < 16; ++i) t.p[i] = d[base[circle_dy(i) + 3] + circle_dx(i)];
+    t.c = d[base[3]];
+    return t;
+}
+
+template <int NMS, int N, int LC, typename ScoreT>
+__device__ __forceinline__ void sweep_evaluate(const SweepShared& sh, UnitCtx& u,
+                                               const LerpConsts& lk, const PendingTest& t) {
+    const int y = (int)(t.code >> 10), cl = (int)(t.code & 1023u);
+    const int x = u.S - LC + cl;
     bool kb, kd;
-    lane_segment_test<N>(c, p, lk, kb, kd);
-    const bool is_kp = act && (kb || kd);
-    const bool owned = cl >= 16 && cl < 16 + kStripCols && y >= u.r0 && y < u.r1;
+    lane_segment_test<N>(t.c, t.p, lk, kb, kd);
+    const bool is_kp = t.act && (kb || kd);
+    const bool owned = cl >= LC && cl < LC + strip_cols(LC) && y >= u.r0 && y < u.r1;
     if constexpr (NMS == kNmsOff) {
         if (is_kp && owned)
             atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
     } else {
         if (is_kp) {
             const uint32_t score = NMS == kNmsMaxThreshold
-                                       ? score_max_threshold<N>(c, p, kd)
-                                       : score_sum_abs(c, p, u.t);
-            *ring_at<ScoreT>(sh, y, cl) = (ScoreT)score;
+                                       ? score_max_threshold<N>(t.c, t.p, kd)
+                                       : score_sum_abs(t.c, t.p, u.t);
+            *ring_at<LC, ScoreT>(sh, y, cl) = (ScoreT)score;
         }
         const bool add = is_kp && owned;
         const uint64_t bal = wave_ballot(add);
         if (add) {
             const uint32_t k = u.kpn + lanes_below(bal);
-            if (k < kSweepKpCap) sh.kp[k] = code;
+            if (k < kSweepKpCap) sh.kp[k] = t.code;
         }
         u.kpn += (uint32_t)__popcll(bal);
     }
 }
 
-template <typename ScoreT>
+template <int NMS, int N, int LC, typename ScoreT>
+__device__ __forceinline__ void sweep_test(const SweepShared& sh, UnitCtx& u,
+                                           const LerpConsts& lk, const uint32_t* pq,
+                                           uint32_t count) {
+    sweep_evaluate<NMS, N, LC, ScoreT>(sh, u, lk, sweep_gather<LC>(sh, u, pq, count));
+}
+
+// 3x3 strict maximum (src/fast_simd.rs:596-615).  All nine reads are issued before any
+// compare (no short-circuit), so they cost one LDS round trip, not nine.
+template <int LC, typename ScoreT>
 __device__ __forceinline__ bool nms_keep_ring(const SweepShared& sh, int y, int cl) {
-    const uint32_t v = *ring_at<ScoreT>(sh, y, cl);
-    const ScoreT* a = ring_at<ScoreT>(sh, y - 1, cl);
-    const ScoreT* m = ring_at<ScoreT>(sh, y, cl);
-    const ScoreT* b = ring_at<ScoreT>(sh, y + 1, cl);
-    return v > a[-1] && v > a[0] && v > a[1] && v > m[-1] && v > m[1] && v > b[-1] &&
-           v > b[0] && v > b[1];
+    const ScoreT* a = ring_at<LC, ScoreT>(sh, y - 1, cl);
+    const ScoreT* m = ring_at<LC, ScoreT>(sh, y, cl);
+    const ScoreT* b = ring_at<LC, ScoreT>(sh, y + 1, cl);
+    const uint32_t v = m[0];
+    const uint32_t n0 = a[-1], n1 = a[0], n2 = a[1], n3 = m[-1], n4 = m[1], n5 = b[-1],
+                   n6 = b[0], n7 = b[1];
+    const uint32_t mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+    return v > mx;
 }
 
 // NMS: keep-bits for the unit's keypoints in rows <= ylim (all their neighbours scored).
-template <typename ScoreT>
+template <int LC, typename ScoreT>
 __device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u, int ylim,
                                                int first_unfinal) {
     const int H = (int)u.src.H;
@@ -174,11 +213,11 @@ __device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u
         for (int y = lo; y <= ylim && y < u.r1; ++y) {
             if (y == 3 || y == H - 4) continue;
             if (u.lane < 1 || u.lane > 62) continue;
-            for (int j = 0; j < 16; ++j) {
-                const int cl = (int)u.lane * 16 + j;
-                const int x = u.S - 16 + cl;
+            for (int j = 0; j < LC; ++j) {
+                const int cl = (int)u.lane * LC + j;
+                const int x = u.S - LC + cl;
                 if (x < 3 || x >= (int)u.src.W - 3) continue;
-                if (*ring_at<ScoreT>(sh, y, cl) != 0 && nms_keep_ring<ScoreT>(sh, y, cl))
+                if (*ring_at<LC, ScoreT>(sh, y, cl) != 0 && nms_keep_ring<LC, ScoreT>(sh, y, cl))
                     atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
             }
         }
@@ -196,32 +235,27 @@ __device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u
         const uint64_t bal = wave_ballot(carry);
         if (carry) sh.kp[kept + lanes_below(bal)] = e;   // kept + idx <= i: read before write
         kept += (uint32_t)__popcll(bal);
-        if (fin && y != 3 && y != H - 4 && nms_keep_ring<ScoreT>(sh, y, cl)) {
-            const int x = u.S - 16 + cl;
+        if (fin && y != 3 && y != H - 4 && nms_keep_ring<LC, ScoreT>(sh, y, cl)) {
+            const int x = u.S - LC + cl;
             atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
         }
     }
     u.kpn = kept;
 }
 
-// Test whatever is queued (a partial batch): the data ring is about to drop rows.
-template <int NMS, int N, typename ScoreT>
-__device__ __forceinline__ void sweep_drain(const SweepShared& sh, UnitCtx& u,
-                                            const LerpConsts& lk) {
-    if (u.pcount > 0 && !(u.flags & kFlagNoFullTest)) sweep_test<NMS, N, ScoreT>(sh, u, lk, sh.pq, u.pcount);
-    u.pcount = 0;
-}
-
-// Horizontal/vertical comparison flags of one row (bit 7 of each byte, 16 pixels).
+// Horizontal/vertical comparison flags of one lane row (bit 7 of each byte, LC pixels).
+template <int LC>
 struct RowFlags {
-    u32x4 b, nd;
+    typename LaneRow<LC>::type b, nd;
 };
 
-__device__ __forceinline__ RowFlags compare_rows(const u32x4& x, const u32x4& nc,
-                                                 const LerpConsts& k) {
-    RowFlags f;
+template <int LC>
+__device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>::type& x,
+                                                     const typename LaneRow<LC>::type& nc,
+                                                     const LerpConsts& k) {
+    RowFlags<LC> f;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < LC / 4; ++m) {
         f.b[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rb), k.kb, 0);   // x - c > t
         f.nd[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rd), k.kd, 0);  // NOT(x - c < -t)
     }
@@ -231,21 +265,24 @@ __device__ __forceinline__ RowFlags compare_rows(const u32x4& x, const u32x4& nc
 template <int NMS, int N, bool EXACT>
 __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     using ScoreT = typename std::conditional<NMS == kNmsSumAbsolute, uint16_t, uint8_t>::type;
+    constexpr int LC = lane_cols_for(NMS);
+    constexpr int M = LC / 4;
+    using RowV = typename LaneRow<LC>::type;
     const uint32_t lane = u.lane;
     const int H = (int)u.src.H, W = (int)u.src.W;
-    const int xb = u.S - 16 + 16 * (int)lane;
+    const int xb = u.S - LC + LC * (int)lane;
     // candidate columns of this lane: owned centres, plus for NMS the two border columns the
     // strip's edge keypoints compare against (scores only)
-    u32x4 vmask;
+    RowV vmask;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < M; ++m) {
         uint32_t v = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int x = xb + 4 * m + j;
             bool ok = x >= 3 && x < W - 3;
             if (lane == 0) ok = ok && NMS != kNmsOff && x == u.S - 1;
-            if (lane == 63) ok = ok && NMS != kNmsOff && x == u.S + kStripCols;
+            if (lane == 63) ok = ok && NMS != kNmsOff && x == u.S + strip_cols(LC);
             if (ok) v |= 0x80u << (8 * j);
         }
         vmask[m] = v;
@@ -255,123 +292,152 @@ __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& 
     const int ys = p0 - 3;                             // first row of vertical comparisons
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
     u.ys = ys;
+    u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
     u.pcount = 0;
     u.kpn = 0;
     u.dense = false;
     int first_unfinal = u.r0;
-    u32x4* ring = reinterpret_cast<u32x4*>(sh.data) + lane;   // + slot * 64
+    RowV* ring = reinterpret_cast<RowV*>(sh.data) + lane;   // + slot * 64
 
     // Prologue: rows ys..ys+2 straight to the LDS ring, rows ys+3..ys+10 into the queue.
-    u32x4 C[4];                                        // rows yv..yv+3, slot (row - ys) & 3
-    u32x4 Q[kSweepPrefetch];                           // row ys+k+3 (+8m) in slot (k+3) & 7
+    RowV C[4];                                         // rows yv..yv+3, slot (row - ys) & 3
+    RowV Q[kSweepPrefetch];                            // row ys+k+3 (+8m) in slot (k+3) & 7
 #pragma unroll
-    for (int k = 0; k < 3; ++k) C[k] = load_row<EXACT>(u.src, ys + k, xb);
+    for (int k = 0; k < 3; ++k) C[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
 #pragma unroll
-    for (int k = 0; k < kSweepPrefetch; ++k) Q[(k + 3) & 7] = load_row<EXACT>(u.src, ys + 3 + k, xb);
+    for (int k = 0; k < kSweepPrefetch; ++k)
+        Q[(k + 3) & 7] = load_row<LC, EXACT>(u.src, ys + 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < 3; ++k) ring[k * 64] = C[k];
-    RowFlags V[4];                                     // vertical flags, slot (row-ys) & 3
+    RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 
-#define FDF_SWEEP_STEP(J)                                                                    \
+    // Step J in two halves.  A: next row load, ring write, comparisons and the pre-filter of
+    // row yv (pure VALU but for the ring write).  B: fresh score row and enqueue (with a full
+    // 64-pixel test whenever the queue fills).
+#define FDF_SWEEP_A(J)                                                                       \
+    const int yv##J = ys + i0 + (J);                                                         \
+    RowV cand##J = (RowV)(0u);                                                               \
     {                                                                                        \
-        const int i = i0 + (J);                                                              \
-        const int yv = ys + i;                                                               \
-        const u32x4 s = Q[((J) + 3) & 7];                  /* row yv + 3 */                  \
+        const int yv = yv##J;                                                                \
+        const RowV s = Q[((J) + 3) & 7];                   /* row yv + 3 */                  \
         ring[(((J) + 3) & 7) * 64] = s;                                                      \
-        Q[((J) + 3) & 7] = load_row<EXACT>(u.src, yv + 3 + kSweepPrefetch, xb);                     \
+        Q[((J) + 3) & 7] = load_row<LC, EXACT>(u.src, yv + 3 + kSweepPrefetch, xb);          \
         C[((J) + 3) & 3] = s;                                                                \
-        const u32x4 c = C[(J) & 3];                                                          \
-        const u32x4 nc = ~c;                                                                 \
-        V[(J) & 3] = compare_rows(s, nc, lk);                                                \
-        if (yv >= p0 && yv < p1 && !(u.flags & kFlagNoLoad)) {                               \
-            if constexpr (NMS != kNmsOff) {                                                  \
+        const RowV c = C[(J) & 3];                                                           \
+        const RowV nc = ~c;                                                                  \
+        V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
+        if (yv >= p0 && yv < p1 && yv >= 3 && yv < H - 3 && !(u.flags & kFlagNoLoad)) {      \
+            RowV e;                                                                          \
+            _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
+            e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
+            const RowFlags<LC> h = compare_rows<LC>(e, nc, lk);                              \
+            const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
+            const RowFlags<LC>& vs = V[(J) & 3];                                             \
+            const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
+            _Pragma("unroll") for (int m = 0; m < M; ++m) {                                  \
+                const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);              \
+                const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);          \
+                const uint32_t bn = ~vn.nd[m], bs = vs.b[m], be = h.b[m], bw = ~hndw;        \
+                const uint32_t dn = ~vn.b[m], ds = vs.nd[m], de = h.nd[m], dw = ~hbw;        \
+                uint32_t br, nd;                                                             \
+                if constexpr (N < 12) {                                                      \
+                    br = (bn | bs) & (be | bw);                                              \
+                    nd = (dn & ds) | (de & dw);                                              \
+                } else {                                                                     \
+                    br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
+                    nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
+                }                                                                            \
+                cand##J[m] = (br | ~nd) & vmask[m];                                          \
+            }                                                                                \
+        }                                                                                    \
+    }
+
+#define FDF_SWEEP_B(J)                                                                       \
+    {                                                                                        \
+        const int yv = yv##J;                                                                \
+        if constexpr (NMS != kNmsOff) {                                                      \
+            if (yv >= p0 && yv < p1) {                                                       \
                 /* fresh ring row: scores default to 0 */                                    \
-                ScoreT* rp = ring_at<ScoreT>(sh, yv, 16 * (int)lane);                        \
-                if constexpr (sizeof(ScoreT) == 1) *reinterpret_cast<u32x4*>(rp) = u32x4{0, 0, 0, 0}; \
-                else { reinterpret_cast<u32x4*>(rp)[0] = u32x4{0, 0, 0, 0};                  \
-                       reinterpret_cast<u32x4*>(rp)[1] = u32x4{0, 0, 0, 0}; }                \
-            }                                                                                \
-            if (yv >= 3 && yv < H - 3) {                                                     \
-                u32x4 e;                                                                     \
-                e[0] = alignbyte(c[1], c[0], 3);                                             \
-                e[1] = alignbyte(c[2], c[1], 3);                                             \
-                e[2] = alignbyte(c[3], c[2], 3);                                             \
-                e[3] = alignbyte(from_next_lane(c[0]), c[3], 3);                             \
-                const RowFlags h = compare_rows(e, nc, lk);                                  \
-                const uint32_t pb = from_prev_lane(h.b[3]), pnd = from_prev_lane(h.nd[3]);   \
-                const RowFlags& vs = V[(J) & 3];                                             \
-                const RowFlags& vn = V[((J) + 1) & 3];                                       \
-                u32x4 cand;                                                                  \
-                _Pragma("unroll") for (int m = 0; m < 4; ++m) {                              \
-                    const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);          \
-                    const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);      \
-                    const uint32_t bn = ~vn.nd[m], bs = vs.b[m], be = h.b[m], bw = ~hndw;    \
-                    const uint32_t dn = ~vn.b[m], ds = vs.nd[m], de = h.nd[m], dw = ~hbw;    \
-                    uint32_t br, nd;                                                         \
-                    if constexpr (N < 12) {                                                  \
-                        br = (bn | bs) & (be | bw);                                          \
-                        nd = (dn & ds) | (de & dw);                                          \
-                    } else {                                                                 \
-                        br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                  \
-                        nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                \
-                    }                                                                        \
-                    cand[m] = (br | ~nd) & vmask[m];                                         \
-                }                                                                            \
-                /* candidate pixels straight into the pixel queue, one per lane per round: */\
-                /* column 4m + j of the lane at bit 8j + m */                                \
-                uint32_t cm = (cand[0] >> 7) | (cand[1] >> 6) | (cand[2] >> 5) | (cand[3] >> 4); \
-                for (;;) {                                                                   \
-                    const bool has = cm != 0;                                                \
-                    const uint64_t bal = wave_ballot(has);                                   \
-                    if (bal == 0) break;                                                     \
-                    if (has) {                                                               \
-                        const uint32_t b = (uint32_t)__builtin_ctz(cm);                      \
-                        const uint32_t col = 4 * (b & 7u) + (b >> 3);                        \
-                        sh.pq[u.pcount + lanes_below(bal)] =                                 \
-                            ((uint32_t)yv << 10) | (16 * lane + col);                        \
-                        cm &= cm - 1;                                                        \
-                    }                                                                        \
-                    u.pcount += (uint32_t)__popcll(bal);                                     \
-                    if (u.pcount >= 64) {                                                    \
-                        u.pcount -= 64;                                                      \
-                        if (!(u.flags & kFlagNoFullTest))                                    \
-                            sweep_test<NMS, N, ScoreT>(sh, u, lk, sh.pq + u.pcount, 64);     \
-                    }                                                                        \
-                }                                                                            \
+                RowV* rp = reinterpret_cast<RowV*>(ring_at<LC, ScoreT>(sh, yv, LC * (int)lane)); \
+                _Pragma("unroll") for (int q = 0; q < (int)sizeof(ScoreT); ++q) rp[q] = (RowV)(0u); \
             }                                                                                \
         }                                                                                    \
-        if (((J) & 1) == 0 && i >= 4) {                                                      \
-            /* rows <= yv are queued and the data ring holds yv-4..yv+3: test them all;      \
-               NMS finalizes rows <= yv-1 */                                                 \
-            sweep_drain<NMS, N, ScoreT>(sh, u, lk);                                          \
-            if constexpr (NMS != kNmsOff) {                                                  \
-                sweep_finalize<ScoreT>(sh, u, yv - 1, first_unfinal);                        \
-                first_unfinal = yv;                                                          \
+        /* candidate pixels straight into the pixel queue, one per lane per round: */        \
+        /* column 4m + j of the lane at bit 8j + m */                                        \
+        uint32_t cm = 0;                                                                     \
+        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= cand##J[m] >> (7 - m);           \
+        for (;;) {                                                                           \
+            const bool has = cm != 0;                                                        \
+            const uint64_t bal = wave_ballot(has);                                           \
+            if (bal == 0) break;                                                             \
+            if (has) {                                                                       \
+                const uint32_t b = (uint32_t)__builtin_ctz(cm);                              \
+                const uint32_t col = 4 * (b & 7u) + (b >> 3);                                \
+                sh.pq[u.pcount + lanes_below(bal)] = ((uint32_t)yv << 10) | (LC * lane + col); \
+                cm &= cm - 1;                                                                \
+            }                                                                                \
+            u.pcount += (uint32_t)__popcll(bal);                                             \
+            if (u.pcount >= 64) {                                                            \
+                u.pcount -= 64;                                                              \
+                if (!(u.flags & kFlagNoFullTest))                                            \
+                    sweep_test<NMS, N, LC, ScoreT>(sh, u, lk, sh.pq + u.pcount, 64);         \
             }                                                                                \
         }                                                                                    \
+    }
+
+    // Every 2 rows (after B(J), J even) the queue is drained, because the data ring is about
+    // to drop a row, and NMS finalizes the rows <= yv(J) - 1.  (Overlapping the drain's LDS
+    // reads with the next row's pre-filter gained 4% but needs ~18 more registers per lane,
+    // which costs half the waves per CU: measured slower.)
+#define FDF_SWEEP_DRAIN(J)                                                                   \
+    if ((i0 + (J) >= 4) && u.pcount > 0 && !(u.flags & kFlagNoFullTest))                    \
+        sweep_test<NMS, N, LC, ScoreT>(sh, u, lk, sh.pq, u.pcount);                          \
+    u.pcount = 0;                                                                            \
+    if constexpr (NMS != kNmsOff) {                                                          \
+        if (i0 + (J) >= 4) {                                                                 \
+            sweep_finalize<LC, ScoreT>(sh, u, yv##J - 1, first_unfinal);                     \
+            first_unfinal = yv##J;                                                           \
+        }                                                                                    \
+    }
+
+#define FDF_SWEEP_PAIR(J, K)                                                                 \
+    {                                                                                        \
+        FDF_SWEEP_A(J)                                                                       \
+        FDF_SWEEP_B(J)                                                                       \
+        FDF_SWEEP_DRAIN(J)                                                                   \
+        FDF_SWEEP_A(K)                                                                       \
+        FDF_SWEEP_B(K)                                                                       \
     }
 
     for (int i0 = 0; i0 < T; i0 += 8) {
-        FDF_SWEEP_STEP(0)
-        FDF_SWEEP_STEP(1)
-        FDF_SWEEP_STEP(2)
-        FDF_SWEEP_STEP(3)
-        FDF_SWEEP_STEP(4)
-        FDF_SWEEP_STEP(5)
-        FDF_SWEEP_STEP(6)
-        FDF_SWEEP_STEP(7)
+        FDF_SWEEP_PAIR(0, 1)
+        FDF_SWEEP_PAIR(2, 3)
+        FDF_SWEEP_PAIR(4, 5)
+        FDF_SWEEP_PAIR(6, 7)
     }
-#undef FDF_SWEEP_STEP
-    // the last block ends on an odd step: at most its last row is still queued, and the
-    // ring still holds the rows it needs (and the score rows, which stop at p1 - 1)
-    sweep_drain<NMS, N, ScoreT>(sh, u, lk);
-    if constexpr (NMS != kNmsOff) sweep_finalize<ScoreT>(sh, u, p1 - 2, first_unfinal);
+#undef FDF_SWEEP_PAIR
+#undef FDF_SWEEP_DRAIN
+#undef FDF_SWEEP_B
+#undef FDF_SWEEP_A
+    // the last block ends on an odd step: at most its row is still queued, and the rings
+    // still hold the rows it needs (the score rows stop at p1 - 1)
+    if (u.pcount > 0 && !(u.flags & kFlagNoFullTest))
+        sweep_test<NMS, N, LC, ScoreT>(sh, u, lk, sh.pq, u.pcount);
+    u.pcount = 0;
+    if constexpr (NMS != kNmsOff) sweep_finalize<LC, ScoreT>(sh, u, p1 - 2, first_unfinal);
 }
 
+// Occupancy target: 4 workgroups (16 waves) per CU, registers <= 128 VGPRs.
+template <int NMS>
+constexpr int sweep_waves_per_eu() { return 4; }
+
 template <int NMS, int N>
-__global__ __launch_bounds__(kThreads) void fast_sweep_kernel(BandParams P) {
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(sweep_waves_per_eu<NMS>(), sweep_waves_per_eu<NMS>())))
+void fast_sweep_kernel(BandParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, score_bytes_for(NMS));
+    constexpr int LC = lane_cols_for(NMS);
+    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, score_bytes_for(NMS), LC);
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
@@ -432,9 +498,9 @@ __global__ __launch_bounds__(kThreads) void fast_sweep_kernel(BandParams P) {
             unit = __builtin_amdgcn_readfirstlane(unit);
             if (unit >= nunits) break;
             const uint32_t strip = unit % P.nstrips, sub = unit / P.nstrips;
-            u.S = (int)(strip * kStripCols);
+            u.S = (int)strip * strip_cols(LC);
             {   // first row whose last lane's window can end past W * H
-                const int last_end = u.S - 16 + 16 * 63 + 16;
+                const int last_end = u.S - LC + LC * 64;
                 const int num = (int)(W * H) - last_end;
                 u.src.tail_row = num < 0 ? 0 : num / (int)W + 1;
             }
@@ -525,7 +591,8 @@ hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream
         default: break;
     }
     if (!fn) return hipErrorInvalidValue;
-    const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, score_bytes_for(nms));
+    const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, score_bytes_for(nms),
+                                            lane_cols_for(nms));
     if (L.total > kSweepMaxLds) return hipErrorInvalidValue;
     if (L.total > kMaxLds) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
