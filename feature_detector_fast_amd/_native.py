@@ -27,8 +27,8 @@ FDF_ERR_ALLOC = 7
 EXPORTED_SYMBOLS = (
     "fdf_abi_version", "fdf_status_string", "fdf_device_count", "fdf_validate",
     "fdf_ctx_create", "fdf_ctx_destroy", "fdf_ctx_stream", "fdf_ctx_set_timing",
-    "fdf_ctx_timing", "fdf_detect", "fdf_detect_batch", "fdf_detect_device",
-    "fdf_score_points",
+    "fdf_ctx_timing", "fdf_detect", "fdf_detect_rgb", "fdf_rgb_to_luma_device",
+    "fdf_detect_batch", "fdf_detect_device", "fdf_score_points",
 )
 
 
@@ -104,6 +104,10 @@ def load():
                                    ctypes.POINTER(ctypes.c_float)]
     lib.fdf_detect.restype = ctypes.c_int
     lib.fdf_detect.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, ctypes.POINTER(sz)]
+    lib.fdf_detect_rgb.restype = ctypes.c_int
+    lib.fdf_detect_rgb.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, ctypes.POINTER(sz)]
+    lib.fdf_rgb_to_luma_device.restype = ctypes.c_int
+    lib.fdf_rgb_to_luma_device.argtypes = [vp, vp, u32, u32, u32, ctypes.c_uint64, vp, vp]
     lib.fdf_detect_batch.restype = ctypes.c_int
     lib.fdf_detect_batch.argtypes = [vp, vp, u32, u32, u32, sz, cfgp, vp, sz, vp,
                                      ctypes.POINTER(sz)]

@@ -23,6 +23,7 @@ struct fdf_ctx {
     std::mutex mu;
     // device workspace, grown on demand
     uint8_t* d_in = nullptr;            size_t in_bytes = 0;       // host-API frame staging
+    uint8_t* d_rgb = nullptr;           size_t rgb_bytes = 0;      // host-API RGB staging
     uint2* d_out = nullptr;             size_t out_points = 0;     // host-API output
     uint64_t* d_offsets = nullptr;      size_t offsets_n = 0;      // host-API frame offsets
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
@@ -102,10 +103,9 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score
     if (const char* e = std::getenv("FDF_NSUB")) g.nsub = (uint32_t)std::strtoul(e, nullptr, 0);
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
-    // LDS per workgroup sets the workgroups per CU: 3 for NMS off (taller bands beat a 4th
-    // workgroup), 4 for max-threshold, 3 for SAD's 16-bit score ring (DESIGN.md §4.1;
-    // tools/ablate.py sweeps).
-    uint32_t budget = score_bytes == 0 ? 48000 : (score_bytes == 2 ? 53000 : 40000);
+    // LDS per workgroup sets the workgroups per CU: 4 without NMS, 3 for max-threshold's
+    // 16-row score ring, 2 for SAD's 16-bit one (tools/ablate.py sweeps).
+    uint32_t budget = score_bytes == 0 ? 40000 : (score_bytes == 1 ? 53000 : 80000);
     if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the
@@ -216,9 +216,11 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
 }
 
 // Shared body of fdf_detect / fdf_detect_batch: host frames in, host points out.
+// `rgb`: the frames are RGB8 (rows of 3 * w bytes at row_stride), converted on the device
+// with image 0.24.6's to_luma8 before detection (src/main.rs:58).
 int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
                 size_t row_stride, size_t frame_stride, const fdf_config* cfg, fdf_point* out,
-                size_t cap, uint64_t* frame_offsets, size_t* n_out) {
+                size_t cap, uint64_t* frame_offsets, size_t* n_out, bool rgb = false) {
     if (!ctx || !n_out || (cap && !out)) return FDF_ERR_ARG;
     int rc = check_config(cfg);
     if (rc) return rc;
@@ -227,7 +229,7 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
     if (rc) return rc;
     if (n_frames == 0) empty = 1;
     if (!data && !empty) return FDF_ERR_ARG;
-    if (row_stride < w) return FDF_ERR_ARG;
+    if (row_stride < (rgb ? 3ull * w : (size_t)w)) return FDF_ERR_ARG;
     if (empty) {
         *n_out = 0;
         if (frame_offsets) std::memset(frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull));
@@ -240,15 +242,26 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
     if ((rc = ensure(&ctx->d_in, &ctx->in_bytes, frame_bytes * n_frames, false, ctx->stream))) return rc;
     if ((rc = ensure(&ctx->d_out, &ctx->out_points, max_points, false, ctx->stream))) return rc;
     if ((rc = ensure(&ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, false, ctx->stream))) return rc;
+    const size_t px = rgb ? 3 : 1;                 // bytes per pixel of the host frames
+    uint8_t* stage = ctx->d_in;
+    if (rgb) {
+        if ((rc = ensure(&ctx->d_rgb, &ctx->rgb_bytes, 3 * frame_bytes * n_frames, false, ctx->stream)))
+            return rc;
+        stage = ctx->d_rgb;
+    }
     for (uint32_t f = 0; f < n_frames; ++f) {
         const uint8_t* src = data + (size_t)f * frame_stride;
-        uint8_t* dst = ctx->d_in + (size_t)f * frame_bytes;
-        hipError_t e = row_stride == w
-                           ? hipMemcpyAsync(dst, src, frame_bytes, hipMemcpyHostToDevice, ctx->stream)
-                           : hipMemcpy2DAsync(dst, w, src, row_stride, w, h, hipMemcpyHostToDevice,
-                                              ctx->stream);
+        uint8_t* dst = stage + (size_t)f * frame_bytes * px;
+        hipError_t e = row_stride == px * w
+                           ? hipMemcpyAsync(dst, src, frame_bytes * px, hipMemcpyHostToDevice,
+                                            ctx->stream)
+                           : hipMemcpy2DAsync(dst, px * w, src, row_stride, px * w, h,
+                                              hipMemcpyHostToDevice, ctx->stream);
         if (e != hipSuccess) return FDF_ERR_DEVICE;
     }
+    if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
+                                        3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
+        return FDF_ERR_DEVICE;
     rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, ctx->d_out, max_points,
                  ctx->d_offsets, ctx->stream);
     if (rc) return rc;
@@ -329,6 +342,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         DeviceGuard guard(ctx->device);
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(ctx->d_in);
+        (void)hipFree(ctx->d_rgb);
         (void)hipFree(ctx->d_out);
         (void)hipFree(ctx->d_offsets);
         (void)hipFree(ctx->d_slots);
@@ -375,6 +389,29 @@ int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t heigh
                size_t* n_out) {
     return detect_host(ctx, data, 1, width, height, stride_bytes, 0, cfg, out, cap, nullptr,
                        n_out);
+}
+
+int fdf_detect_rgb(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+                   size_t stride_bytes, const fdf_config* cfg, fdf_point* out, size_t cap,
+                   size_t* n_out) {
+    return detect_host(ctx, data, 1, width, height, stride_bytes, 0, cfg, out, cap, nullptr,
+                       n_out, true);
+}
+
+int fdf_rgb_to_luma_device(fdf_ctx* ctx, const uint8_t* d_rgb, uint32_t n_frames,
+                           uint32_t width, uint32_t height, uint64_t rgb_frame_stride_bytes,
+                           uint8_t* d_grey, void* stream) {
+    if (!ctx) return FDF_ERR_ARG;
+    const uint64_t pixels = (uint64_t)width * height;
+    if (n_frames == 0 || pixels == 0) return FDF_OK;
+    if (!d_rgb || !d_grey || pixels > 0x7fffffffull / 3 || rgb_frame_stride_bytes < 3 * pixels ||
+        n_frames > 65535u)
+        return FDF_ERR_ARG;
+    DeviceGuard guard(ctx->device);
+    if (fdfk::launch_rgb_to_luma(d_rgb, n_frames, (uint32_t)pixels, rgb_frame_stride_bytes, d_grey,
+                                 reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+        return FDF_ERR_DEVICE;
+    return FDF_OK;
 }
 
 int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t width,

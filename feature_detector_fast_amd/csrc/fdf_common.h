@@ -71,21 +71,32 @@ __device__ __forceinline__ uint32_t gather_flags(const uint32_t (&f)[4]) {
     return __builtin_amdgcn_perm(x, x, 0x02000200u);     // bytes [b0, b2, b0, b2]
 }
 
-// Bright / dark runs of >= N on the ring p (src/fast_simd.rs:115-297): the 16 bytes are
-// packed 4 per word (byte j of word m = pixel 4j + m) and compared with the exact lerp SWAR.
+// Bright / dark runs of >= N (src/fast_simd.rs:115-297) on the ring packed 4 bytes per word
+// (byte j of w[m] = circle pixel 4j + m), compared with the exact lerp SWAR.
 template <int N>
-__device__ __forceinline__ void lane_segment_test(uint32_t c, const uint32_t (&p)[16],
-                                                  const LerpConsts& k, bool& bright, bool& dark) {
+__device__ __forceinline__ void lane_segment_test_packed(uint32_t c, const uint32_t (&w)[4],
+                                                         const LerpConsts& k, bool& bright,
+                                                         bool& dark) {
     const uint32_t nc = ~(c * 0x01010101u);
     uint32_t fb[4], fn[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-        const uint32_t w = p[m] | (p[m + 4] << 8) | (p[m + 8] << 16) | (p[m + 12] << 24);
-        fb[m] = lerp_u8(lerp_u8(w, nc, k.rb), k.kb, 0);   // p - c > t
-        fn[m] = lerp_u8(lerp_u8(w, nc, k.rd), k.kd, 0);   // NOT(p - c < -t)
+        fb[m] = lerp_u8(lerp_u8(w[m], nc, k.rb), k.kb, 0);   // p - c > t
+        fn[m] = lerp_u8(lerp_u8(w[m], nc, k.rd), k.kd, 0);   // NOT(p - c < -t)
     }
     bright = run_of<N>(gather_flags(fb));
     dark = run_of<N>(~gather_flags(fn));
+}
+
+// The same on 16 separate ring bytes.
+template <int N>
+__device__ __forceinline__ void lane_segment_test(uint32_t c, const uint32_t (&p)[16],
+                                                  const LerpConsts& k, bool& bright, bool& dark) {
+    uint32_t w[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        w[m] = p[m] | (p[m + 4] << 8) | (p[m + 8] << 16) | (p[m + 12] << 24);
+    lane_segment_test_packed<N>(c, w, k, bright, dark);
 }
 
 // Max-threshold score of a keypoint (src/fast_simd.rs:623-718, scalar :172-209).  For

@@ -23,19 +23,21 @@ constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compa
 constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
 
 // Column-sweep kernel (fdf_sweep.hip): per-wave LDS region + the band bitmap.
-// Columns per lane: 16 without NMS; 8 with NMS, whose per-wave score ring and keypoint list
-// would otherwise halve the waves per CU.  A strip is 62 lanes wide (lanes 0, 63: halo).
+// Columns per lane: 16 without NMS; 8 with NMS, whose per-wave score ring would otherwise
+// cut the waves per CU.  A strip is 62 lanes wide (lanes 0 and 63 are halo lanes).
 __host__ __device__ constexpr int lane_cols_for(uint32_t nms) { return nms == 0 ? 16 : 8; }
 __host__ __device__ constexpr int strip_cols(int lc) { return 62 * lc; }
-constexpr int kSweepRing = 4;                 // NMS score ring rows per wave (power of two)
-constexpr int kSweepDataRows = 8;             // pixel-row ring per wave read by the full test
-constexpr int kSweepPrefetch = 8;             // rows loaded ahead of the sweep (register queue)
-constexpr int kSweepPixelQ = 128;             // queued candidate pixels per wave (63 + 64)
+constexpr int kSweepPixelQ = 256;             // candidate pixel FIFO per wave (power of two)
+constexpr int kSweepRing = 16;                // NMS score ring rows per wave (power of two)
 constexpr int kSweepKpCap = 256;              // unfinalized NMS keypoints per wave
 constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per workgroup)
 
+// A full-test batch is issued every kSweepIssue(nms) rows once 64 candidates are queued and
+// is evaluated the same number of rows later.
+__host__ __device__ constexpr int sweep_issue_every(uint32_t nms) { return nms == 0 ? 2 : 4; }
+
 struct SweepLayout {
-    uint32_t data, pq, ring, kp, wave_bytes, bitmap, total;
+    uint32_t pq, ring, kp, wave_bytes, bitmap, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t v);
@@ -44,7 +46,6 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
                                                          uint32_t score_bytes, uint32_t lc) {
     SweepLayout L;
     uint32_t o = 0;
-    L.data = o;     o += kSweepDataRows * 64 * lc;
     L.pq = o;       o += kSweepPixelQ * 4;
     L.ring = o;     o += kSweepRing * 64 * lc * score_bytes;
     L.kp = o;       o += score_bytes ? kSweepKpCap * 4 : 0;
@@ -109,6 +110,8 @@ struct CompactParams {
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);
 hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
+hipError_t launch_rgb_to_luma(const uint8_t* rgb, uint32_t n_frames, uint32_t pixels,
+                              uint64_t rgb_frame_stride, uint8_t* grey, hipStream_t stream);
 hipError_t launch_score_points(const uint8_t* img, uint32_t width, const uint2* pts,
                                uint32_t npts, uint32_t nms, uint32_t t, uint32_t n,
                                uint16_t* out, hipStream_t stream);

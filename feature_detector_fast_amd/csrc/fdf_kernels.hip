@@ -6,6 +6,8 @@
 //   groups of bands, then each group copies its bands' points to their final positions.
 // score_points_kernel -- the reference's two NMS score functions on given points
 //   (extension: fdf_score_points).
+// rgb_to_luma_kernel -- RGB8 -> grey exactly as image 0.24.6's to_luma8, which the
+//   reference's callers apply before detect (src/main.rs:58, tests/compare.rs:33).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -235,6 +237,66 @@ hipError_t launch_score_points(const uint8_t* img, uint32_t W, const uint2* pts,
     if (npts == 0) return hipSuccess;
     hipLaunchKernelGGL(score_points_kernel, dim3((npts + 255) / 256), dim3(256), 0, stream,
                        img, W, pts, npts, nms, t, n, out);
+    return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------------------
+// RGB8 -> grey: image 0.24.6 color.rs rgb_to_luma for u8 (not vendored in the reference;
+// its published formula): l = 2126 r + 7152 g + 722 b, luma = l / 10000 (truncating).
+// 16 pixels per thread: three 16-byte loads, one 16-byte store; only a frame's last,
+// partial group goes byte by byte, so nothing outside the frame is read or written.
+// ---------------------------------------------------------------------------------------
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t luma_of(uint32_t r, uint32_t g, uint32_t b) {
+    return (2126u * r + 7152u * g + 722u * b) / 10000u;
+}
+
+__global__ __launch_bounds__(256) void rgb_to_luma_kernel(const uint8_t* rgb,
+                                                          uint64_t rgb_frame_stride,
+                                                          uint32_t pixels, uint8_t* grey) {
+    const uint32_t g = blockIdx.x * 256u + threadIdx.x;        // 16-pixel group
+    const uint32_t first = g * 16u;
+    if (first >= pixels) return;
+    const uint8_t* src = rgb + (uint64_t)blockIdx.y * rgb_frame_stride;
+    uint8_t* dst = grey + (uint64_t)blockIdx.y * pixels;
+    if (first + 16u > pixels) {
+        for (uint32_t i = first; i < pixels; ++i)
+            dst[i] = (uint8_t)luma_of(src[3 * i], src[3 * i + 1], src[3 * i + 2]);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t in = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(src), 0, (int)(3u * pixels), 0x00020000);
+    const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)pixels,
+                                                                          0x00020000);
+    uint32_t w[12];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const u32x4_t v = __builtin_bit_cast(
+            u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(in, (int)(3u * first) + 16 * k, 0, 0));
+#pragma unroll
+        for (int m = 0; m < 4; ++m) w[4 * k + m] = v[m];
+    }
+    u32x4_t o = (u32x4_t)(0u);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t r = (w[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 0xffu;
+        const uint32_t gg = (w[(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 0xffu;
+        const uint32_t b = (w[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 0xffu;
+        o[j >> 2] |= luma_of(r, gg, b) << (8 * (j & 3));
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(o, out, (int)first, 0, 0);
+}
+
+hipError_t launch_rgb_to_luma(const uint8_t* rgb, uint32_t n_frames, uint32_t pixels,
+                              uint64_t rgb_frame_stride, uint8_t* grey, hipStream_t stream) {
+    if (n_frames == 0 || pixels == 0) return hipSuccess;
+    const uint32_t groups = (pixels + 15u) / 16u;
+    const dim3 grid((groups + 255u) / 256u, n_frames);
+    if (n_frames > 65535u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rgb_to_luma_kernel, grid, dim3(256), 0, stream, rgb, rgb_frame_stride,
+                       pixels, grey);
     return hipGetLastError();
 }
 

@@ -4,30 +4,32 @@
 // determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
 //
 // One workgroup (4 waves) owns a band of R full-width centre rows of one frame.  The band is
-// cut into units = (column strip) x (sub-band of rows); a wave sweeps a unit top to bottom
-// (DESIGN.md §4.1):
+// cut into units = (column strip) x (sub-band of rows); waves take units from an LDS counter
+// and sweep them top to bottom:
 //   * lane l owns LC columns (one LC-byte buffer load per row; LC = 16 without NMS, 8 with
-//     NMS, whose score ring and keypoint list would otherwise halve the waves per CU); lanes
-//     0 and 63 are halo lanes that only feed their neighbours, so a strip covers 62 x LC
-//     centres;
-//   * pixel rows stream through an 8-deep register queue (loads run 8 rows ahead, never
-//     guarded by a branch, so the prefetch stays in flight), then into a per-wave LDS ring of
-//     the last 8 rows that the full test reads;
+//     NMS, whose score ring would otherwise cut the waves per CU); lanes 0 and 63 are halo
+//     lanes that only feed their neighbours, so a strip covers 62 x LC centres;
+//   * pixel rows stream through an 8-slot register ring: loads run 4 rows ahead, are never
+//     guarded by a branch and are never copied, so the compiler's vmcnt bookkeeping keeps
+//     them in flight;
 //   * every pairwise comparison is made once and used by both of its pixels: the vertical
 //     pair (I(y), I(y+3)) gives S-flags for row y and N-flags for row y+3, the horizontal
 //     pair (I(x), I(x+3)) gives E-flags for x and W-flags for x+3 (a 3-byte shift, with the
 //     neighbouring lane's bytes via DPP).  Comparisons are byte-SWAR v_lerp_u8 (exact per
 //     byte, see fdf_common.h), so the cardinal pre-filter (src/fast_simd.rs:441-509) costs
-//     2 lerps per pixel instead of 4;
-//   * candidate pixels go straight into a per-wave queue (one per lane per round) and are
-//     tested 64 at a time, one pixel per lane, with the VALU segment test of fdf_common.h on
-//     bytes read from the LDS ring (no global loads outside the row stream); every 2 rows
-//     the queue is drained, since the ring is about to drop the oldest row;
-//   * NMS: scores live in a 4-row LDS ring per wave; every 2 rows the queue is flushed and
-//     the keypoints of the finished rows pass the 3x3 strict-max test (:589-616) into the
-//     workgroup's band bitmap.
-// The band's keep-bits are then written to its output slot exactly as fdf_kernels.hip's
-// band kernel does, and compact_kernel orders all slots in raster order.
+//     2 lerps per pixel;
+//   * candidate pixels go into a per-wave FIFO in LDS (one per lane per round).  Every
+//     kSweepIssue rows, once 64 are queued, a batch is issued: each lane gathers its pixel's
+//     7x7 neighbourhood with 7 row-window loads straight from the frame (the rows were just
+//     streamed, so these hit L2).  The batch is evaluated kSweepIssue rows later -- by then
+//     the row loads issued before it are due anyway, so waiting for it never drains the row
+//     prefetch -- with the per-lane VALU segment test (fdf_common.h);
+//   * NMS: scores go to a 16-row LDS score ring per wave, keypoints of owned pixels to a
+//     list; whenever testing has caught up with more rows, the keypoints of the rows whose
+//     neighbours are all scored pass the 3x3 strict-max test (:589-616) into the workgroup's
+//     band bitmap.
+// The band's keep-bits are then written to its output slot (its points in raster order, or
+// the bitmap if they do not fit) and compact_kernel orders all slots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -96,9 +98,8 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
 }
 
 struct SweepShared {
-    uint8_t* data;         // kSweepDataRows x 64*LC pixel bytes, slot (row - ys) & 7
-    uint32_t* pq;          // kSweepPixelQ: (row << 10) | strip column
-    void* ring;            // kSweepRing x 64*LC scores (NMS)
+    uint32_t* pq;          // kSweepPixelQ FIFO of (row << 10) | strip column
+    void* ring;            // kSweepRing x 64*LC scores (NMS), row y in slot y & 15
     uint32_t* kp;          // kSweepKpCap: (row << 10) | strip column
     uint32_t* bitmap;      // band keep-bits, R x words_per_row
 };
@@ -109,10 +110,10 @@ struct UnitCtx {
     int S;                 // first owned centre column of the strip
     int r0, r1;            // owned centre rows of the unit
     int y0;                // first centre row of the band
-    int ys;                // first row of the unit's sweep (data ring slot 0)
     uint32_t lane;
     bool dense;            // NMS keypoint list overflowed: finalize densely
-    uint32_t pcount, kpn;
+    uint32_t head, tail;   // candidate FIFO: entries [head, tail) at pq[i % kSweepPixelQ]
+    uint32_t kpn;
     uint32_t flags;        // BandParams::flags (ablation runs only)
 };
 
@@ -121,70 +122,93 @@ __device__ __forceinline__ ScoreT* ring_at(const SweepShared& sh, int y, int cl)
     return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kSweepRing - 1)) * (64 * LC) + cl;
 }
 
-// Full test of up to 64 queued pixels, one per lane (per-lane VALU segment test,
-// fdf_common.h), in two halves so that the LDS reads of a batch can be in flight while the
-// sweep does other work: gather reads the pixel codes and their 17 bytes from the row ring,
-// evaluate tests them and records keypoints / scores.
-struct PendingTest {
+// ---------------------------------------------------------------------------------------
+// Full test of a batch of up to 64 queued pixels, one per lane, in two halves: issue pops
+// the batch from the FIFO and starts its loads; evaluate tests the pixels (per-lane VALU
+// segment test) and records keypoints / scores.
+// ---------------------------------------------------------------------------------------
+struct Batch {
     uint32_t code;         // (row << 10) | strip column
     bool act;
-    uint32_t c, p[16];
+    uint32_t a0, a6;       // rows y-3, y+3: 4 bytes from x-1
+    u32x2 a1, a5;          // rows y-2, y+2: 8 bytes from x-2
+    u32x2 a2, a3, a4;      // rows y-1, y, y+1: 8 bytes from x-3
 };
 
+// Pops n (<= 64) entries.  n = 0 still issues the loads (all lanes at a harmless address):
+// the pipelined issue points load unconditionally, so that every path through the sweep
+// has the same sequence of loads and the compiler's vmcnt counts stay exact.
 template <int LC>
-__device__ __forceinline__ PendingTest sweep_gather(const SweepShared& sh, const UnitCtx& u,
-                                                    const uint32_t* pq, uint32_t count) {
-    PendingTest t;
-    t.act = u.lane < count;
-    t.code = t.act ? pq[u.lane] : 0u;
-    const int y = (int)(t.code >> 10), cl = (int)(t.code & 1023u);
-    // 7x7 neighbourhood from the LDS row ring: row y+dy in slot (y + dy - ys) & 7
-    const int rel = y - u.ys;
-    const uint8_t* d = sh.data + (t.act ? cl : LC);
-    uint32_t base[7];
-#pragma unroll
-    for (int r = 0; r < 7; ++r)
-        base[r] = (uint32_t)((rel + r - 3) & (kSweepDataRows - 1)) * (64 * LC);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t.p[i] = d[base[circle_dy(i) + 3] + circle_dx(i)];
-    t.c = d[base[3]];
-    return t;
+__device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, uint32_t n) {
+    Batch b;
+    b.act = u.lane < n;
+    b.code = b.act ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
+    u.head += n;
+    const int W = (int)u.src.W;
+    // inactive lanes read around centre (3, 3), which every tested frame has
+    const int y = b.act ? (int)(b.code >> 10) : 3;
+    const int x = b.act ? u.S - LC + (int)(b.code & 1023u) : 3;
+    const int o = (y - 3) * W + x;                              // pixel (x, y - 3)
+    // the windows stay inside the frame: rows y-3 .. y+3 are rows, and the 1-2 bytes past
+    // a row end (rows y-1 .. y+2 only) belong to the next row
+    b.a0 = __builtin_amdgcn_raw_buffer_load_b32(u.src.rs, o - 1, 0, 0);
+    b.a1 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 2, W, 0));
+    b.a2 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 3, 2 * W, 0));
+    b.a3 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 3, 3 * W, 0));
+    b.a4 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 3, 4 * W, 0));
+    b.a5 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 2, 5 * W, 0));
+    b.a6 = __builtin_amdgcn_raw_buffer_load_b32(u.src.rs, o - 1, 6 * W, 0);
+    return b;
+}
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// The ring packed 4 bytes per word (byte j of w[m] = circle pixel 4j + m) and the centre.
+// Circle pixels by window byte: a0 = {15, 0, 1} at bytes 0-2; a1 = {14 @0, 2 @4};
+// a2 = {13 @0, 3 @6}; a3 = {12 @0, c @3, 4 @6}; a4 = {11 @0, 5 @6}; a5 = {10 @0, 6 @4};
+// a6 = {9, 8, 7} at bytes 0-2.  perm selector bytes: 0-3 = low source, 4-7 = high source,
+// 0x0c = zero.
+__device__ __forceinline__ void pack_ring(const Batch& b, uint32_t (&w)[4], uint32_t& c) {
+    w[0] = perm(b.a3.y, b.a0, 0x0c0c0601u) | perm(b.a3.x, b.a6, 0x04010c0cu);   // 0 4 8 12
+    w[1] = perm(b.a4.y, b.a0, 0x0c0c0602u) | perm(b.a2.x, b.a6, 0x04000c0cu);   // 1 5 9 13
+    w[2] = perm(b.a1.y, b.a1.x, 0x000c0c04u) | perm(b.a5.y, b.a5.x, 0x0c00040cu); // 2 6 10 14
+    w[3] = perm(b.a6, b.a2.y, 0x0c0c0602u) | perm(b.a0, b.a4.x, 0x04000c0cu);   // 3 7 11 15
+    c = b.a3.x >> 24;
 }
 
 template <int NMS, int N, int LC, typename ScoreT>
-__device__ __forceinline__ void sweep_evaluate(const SweepShared& sh, UnitCtx& u,
-                                               const LerpConsts& lk, const PendingTest& t) {
-    const int y = (int)(t.code >> 10), cl = (int)(t.code & 1023u);
+__device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
+                                               const LerpConsts& lk, const Batch& b) {
+    const int y = (int)(b.code >> 10), cl = (int)(b.code & 1023u);
     const int x = u.S - LC + cl;
+    uint32_t w[4], c;
+    pack_ring(b, w, c);
     bool kb, kd;
-    lane_segment_test<N>(t.c, t.p, lk, kb, kd);
-    const bool is_kp = t.act && (kb || kd);
+    lane_segment_test_packed<N>(c, w, lk, kb, kd);
+    const bool is_kp = b.act && (kb || kd);
     const bool owned = cl >= LC && cl < LC + strip_cols(LC) && y >= u.r0 && y < u.r1;
     if constexpr (NMS == kNmsOff) {
         if (is_kp && owned)
             atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
     } else {
         if (is_kp) {
-            const uint32_t score = NMS == kNmsMaxThreshold
-                                       ? score_max_threshold<N>(t.c, t.p, kd)
-                                       : score_sum_abs(t.c, t.p, u.t);
+            uint32_t p[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+            const uint32_t score = NMS == kNmsMaxThreshold ? score_max_threshold<N>(c, p, kd)
+                                                           : score_sum_abs(c, p, u.t);
             *ring_at<LC, ScoreT>(sh, y, cl) = (ScoreT)score;
         }
         const bool add = is_kp && owned;
         const uint64_t bal = wave_ballot(add);
         if (add) {
             const uint32_t k = u.kpn + lanes_below(bal);
-            if (k < kSweepKpCap) sh.kp[k] = t.code;
+            if (k < kSweepKpCap) sh.kp[k] = b.code;
         }
         u.kpn += (uint32_t)__popcll(bal);
     }
-}
-
-template <int NMS, int N, int LC, typename ScoreT>
-__device__ __forceinline__ void sweep_test(const SweepShared& sh, UnitCtx& u,
-                                           const LerpConsts& lk, const uint32_t* pq,
-                                           uint32_t count) {
-    sweep_evaluate<NMS, N, LC, ScoreT>(sh, u, lk, sweep_gather<LC>(sh, u, pq, count));
 }
 
 // 3x3 strict maximum (src/fast_simd.rs:596-615).  All nine reads are issued before any
@@ -201,15 +225,15 @@ __device__ __forceinline__ bool nms_keep_ring(const SweepShared& sh, int y, int 
     return v > mx;
 }
 
-// NMS: keep-bits for the unit's keypoints in rows <= ylim (all their neighbours scored).
+// NMS: keep-bits for the unit's keypoints in rows first .. ylim (all neighbours scored).
 template <int LC, typename ScoreT>
-__device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u, int ylim,
-                                               int first_unfinal) {
+__device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u, int first,
+                                               int ylim) {
     const int H = (int)u.src.H;
     if (u.kpn > kSweepKpCap) u.dense = true;
     if (u.dense) {
         // rare: the list overflowed -- scan the owned columns of the rows densely
-        const int lo = first_unfinal > u.r0 ? first_unfinal : u.r0;
+        const int lo = first > u.r0 ? first : u.r0;
         for (int y = lo; y <= ylim && y < u.r1; ++y) {
             if (y == 3 || y == H - 4) continue;
             if (u.lane < 1 || u.lane > 62) continue;
@@ -262,11 +286,41 @@ __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>:
     return f;
 }
 
+// Test everything queued, now (FIFO overflow, a score-ring wrap, the end of a unit).
+template <int NMS, int N, int LC, typename ScoreT>
+__device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
+                                            const LerpConsts& lk, bool& inflight,
+                                            const Batch& batch) {
+    if (inflight) {
+        evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, batch);
+        inflight = false;
+    }
+    while (u.tail != u.head) {
+        if (u.flags & kFlagNoFullTest) {
+            u.head = u.tail;
+            break;
+        }
+        const Batch b = issue_batch<LC>(sh, u, min(u.tail - u.head, 64u));
+        evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, b);
+    }
+}
+
+// NMS: finalize the rows first_unfinal .. ylim (when there are any).
+template <int LC, typename ScoreT>
+__device__ __forceinline__ void finalize_upto(const SweepShared& sh, UnitCtx& u,
+                                              int& first_unfinal, int ylim) {
+    if (ylim >= first_unfinal) {
+        sweep_finalize<LC, ScoreT>(sh, u, first_unfinal, ylim);
+        first_unfinal = ylim + 1;
+    }
+}
+
 template <int NMS, int N, bool EXACT>
-__device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
+__device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     using ScoreT = typename std::conditional<NMS == kNmsSumAbsolute, uint16_t, uint8_t>::type;
     constexpr int LC = lane_cols_for(NMS);
     constexpr int M = LC / 4;
+    constexpr int kIssue = sweep_issue_every(NMS);
     using RowV = typename LaneRow<LC>::type;
     const uint32_t lane = u.lane;
     const int H = (int)u.src.H, W = (int)u.src.W;
@@ -291,42 +345,35 @@ __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& 
     const int p0 = u.r0 - ringr, p1 = u.r1 + ringr;   // rows run through the pre-filter
     const int ys = p0 - 3;                             // first row of vertical comparisons
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
-    u.ys = ys;
     u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
-    u.pcount = 0;
+    u.head = u.tail = 0;
     u.kpn = 0;
     u.dense = false;
-    int first_unfinal = u.r0;
-    RowV* ring = reinterpret_cast<RowV*>(sh.data) + lane;   // + slot * 64
+    int first_unfinal = u.r0;                          // NMS: rows before it are finalized
+    bool inflight = false;
+    Batch batch;
 
-    // Prologue: rows ys..ys+2 straight to the LDS ring, rows ys+3..ys+10 into the queue.
-    RowV C[4];                                         // rows yv..yv+3, slot (row - ys) & 3
-    RowV Q[kSweepPrefetch];                            // row ys+k+3 (+8m) in slot (k+3) & 7
+    // One 8-slot ring of pixel rows: row r in slot (r - ys) & 7.  At step J (row yv) it holds
+    // rows yv .. yv+6 with yv+4 .. yv+6 still loading, and row yv+7 is loaded into the slot
+    // of row yv-1, which is dead.  Nothing is copied, so every slot keeps its registers
+    // across loop iterations and no wait is needed for a register move.
+    RowV Rw[8];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) C[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
-#pragma unroll
-    for (int k = 0; k < kSweepPrefetch; ++k)
-        Q[(k + 3) & 7] = load_row<LC, EXACT>(u.src, ys + 3 + k, xb);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ring[k * 64] = C[k];
+    for (int k = 0; k < 7; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 
-    // Step J in two halves.  A: next row load, ring write, comparisons and the pre-filter of
-    // row yv (pure VALU but for the ring write).  B: fresh score row and enqueue (with a full
-    // 64-pixel test whenever the queue fills).
-#define FDF_SWEEP_A(J)                                                                       \
-    const int yv##J = ys + i0 + (J);                                                         \
-    RowV cand##J = (RowV)(0u);                                                               \
+    // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
+#define FDF_SWEEP_STEP(J)                                                                    \
     {                                                                                        \
-        const int yv = yv##J;                                                                \
-        const RowV s = Q[((J) + 3) & 7];                   /* row yv + 3 */                  \
-        ring[(((J) + 3) & 7) * 64] = s;                                                      \
-        Q[((J) + 3) & 7] = load_row<LC, EXACT>(u.src, yv + 3 + kSweepPrefetch, xb);          \
-        C[((J) + 3) & 3] = s;                                                                \
-        const RowV c = C[(J) & 3];                                                           \
+        const int yv = ys + i0 + (J);                                                        \
+        RowV cand = (RowV)(0u);                                                              \
+        Rw[((J) + 7) & 7] = load_row<LC, EXACT>(u.src, yv + 7, xb);                          \
+        const RowV s = Rw[((J) + 3) & 7];                  /* row yv + 3 */                  \
+        const RowV c = Rw[(J) & 7];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
-        if (yv >= p0 && yv < p1 && yv >= 3 && yv < H - 3 && !(u.flags & kFlagNoLoad)) {      \
+        const bool live = yv >= p0 && yv < p1;                                               \
+        if (live && yv >= 3 && yv < H - 3 && !(u.flags & kFlagNoLoad)) {                     \
             RowV e;                                                                          \
             _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
             e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
@@ -347,84 +394,77 @@ __device__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& 
                     br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
                     nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
                 }                                                                            \
-                cand##J[m] = (br | ~nd) & vmask[m];                                          \
+                cand[m] = (br | ~nd) & vmask[m];                                             \
             }                                                                                \
         }                                                                                    \
-    }
-
-#define FDF_SWEEP_B(J)                                                                       \
-    {                                                                                        \
-        const int yv = yv##J;                                                                \
         if constexpr (NMS != kNmsOff) {                                                      \
-            if (yv >= p0 && yv < p1) {                                                       \
-                /* fresh ring row: scores default to 0 */                                    \
+            if (live) {                                                                      \
+                /* the ring slot of row yv still holds row yv - 16: if that row is still */  \
+                /* needed as an NMS neighbour, catch testing and NMS up first */             \
+                if (yv - kSweepRing >= first_unfinal - 1) {                                  \
+                    flush_tests<NMS, N, LC, ScoreT>(sh, u, lk, inflight, batch);             \
+                    finalize_upto<LC, ScoreT>(sh, u, first_unfinal, yv - 2);                 \
+                }                                                                            \
                 RowV* rp = reinterpret_cast<RowV*>(ring_at<LC, ScoreT>(sh, yv, LC * (int)lane)); \
                 _Pragma("unroll") for (int q = 0; q < (int)sizeof(ScoreT); ++q) rp[q] = (RowV)(0u); \
             }                                                                                \
         }                                                                                    \
-        /* candidate pixels straight into the pixel queue, one per lane per round: */        \
-        /* column 4m + j of the lane at bit 8j + m */                                        \
+        /* candidate pixels into the FIFO, one per lane per round: column 4m + j of the */   \
+        /* lane is bit 8j + m of cm */                                                       \
         uint32_t cm = 0;                                                                     \
-        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= cand##J[m] >> (7 - m);           \
+        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= cand[m] >> (7 - m);              \
         for (;;) {                                                                           \
             const bool has = cm != 0;                                                        \
             const uint64_t bal = wave_ballot(has);                                           \
             if (bal == 0) break;                                                             \
             if (has) {                                                                       \
-                const uint32_t b = (uint32_t)__builtin_ctz(cm);                              \
-                const uint32_t col = 4 * (b & 7u) + (b >> 3);                                \
-                sh.pq[u.pcount + lanes_below(bal)] = ((uint32_t)yv << 10) | (LC * lane + col); \
+                const uint32_t bit = (uint32_t)__builtin_ctz(cm);                            \
+                const uint32_t col = 4 * (bit & 7u) + (bit >> 3);                            \
+                sh.pq[(u.tail + lanes_below(bal)) & (kSweepPixelQ - 1)] =                    \
+                    ((uint32_t)yv << 10) | (LC * lane + col);                                \
                 cm &= cm - 1;                                                                \
             }                                                                                \
-            u.pcount += (uint32_t)__popcll(bal);                                             \
-            if (u.pcount >= 64) {                                                            \
-                u.pcount -= 64;                                                              \
-                if (!(u.flags & kFlagNoFullTest))                                            \
-                    sweep_test<NMS, N, LC, ScoreT>(sh, u, lk, sh.pq + u.pcount, 64);         \
+            u.tail += (uint32_t)__popcll(bal);                                               \
+            if (u.tail - u.head > kSweepPixelQ - 64) {                                       \
+                /* dense image: test the oldest batch now, synchronously */                  \
+                if (u.flags & kFlagNoFullTest) u.head += 64;                                 \
+                else evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, issue_batch<LC>(sh, u, 64u)); \
             }                                                                                \
         }                                                                                    \
-    }
-
-    // Every 2 rows (after B(J), J even) the queue is drained, because the data ring is about
-    // to drop a row, and NMS finalizes the rows <= yv(J) - 1.  (Overlapping the drain's LDS
-    // reads with the next row's pre-filter gained 4% but needs ~18 more registers per lane,
-    // which costs half the waves per CU: measured slower.)
-#define FDF_SWEEP_DRAIN(J)                                                                   \
-    if ((i0 + (J) >= 4) && u.pcount > 0 && !(u.flags & kFlagNoFullTest))                    \
-        sweep_test<NMS, N, LC, ScoreT>(sh, u, lk, sh.pq, u.pcount);                          \
-    u.pcount = 0;                                                                            \
-    if constexpr (NMS != kNmsOff) {                                                          \
-        if (i0 + (J) >= 4) {                                                                 \
-            sweep_finalize<LC, ScoreT>(sh, u, yv##J - 1, first_unfinal);                     \
-            first_unfinal = yv##J;                                                           \
+        if (((J) % kIssue) == kIssue - 1) {                                                  \
+            /* the batch issued kIssue rows ago is due; issue the next full one */           \
+            if (inflight) {                                                                  \
+                evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, batch);                        \
+                inflight = false;                                                            \
+            }                                                                                \
+            const bool full = u.tail - u.head >= 64;                                         \
+            if (full && (u.flags & kFlagNoFullTest)) u.head += 64;                           \
+            const uint32_t n = (full && !(u.flags & kFlagNoFullTest)) ? 64u : 0u;            \
+            batch = issue_batch<LC>(sh, u, n);                                               \
+            inflight = n != 0;                                                               \
+            if constexpr (NMS != kNmsOff) {                                                  \
+                /* rows before the oldest untested candidate are fully tested */             \
+                int r = yv + 1;                                                              \
+                if (u.tail != u.head) r = (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 10);   \
+                if (inflight) r = min(r, (int)(__builtin_amdgcn_readfirstlane(batch.code) >> 10)); \
+                finalize_upto<LC, ScoreT>(sh, u, first_unfinal, r - 2);                      \
+            }                                                                                \
         }                                                                                    \
-    }
-
-#define FDF_SWEEP_PAIR(J, K)                                                                 \
-    {                                                                                        \
-        FDF_SWEEP_A(J)                                                                       \
-        FDF_SWEEP_B(J)                                                                       \
-        FDF_SWEEP_DRAIN(J)                                                                   \
-        FDF_SWEEP_A(K)                                                                       \
-        FDF_SWEEP_B(K)                                                                       \
     }
 
     for (int i0 = 0; i0 < T; i0 += 8) {
-        FDF_SWEEP_PAIR(0, 1)
-        FDF_SWEEP_PAIR(2, 3)
-        FDF_SWEEP_PAIR(4, 5)
-        FDF_SWEEP_PAIR(6, 7)
+        FDF_SWEEP_STEP(0)
+        FDF_SWEEP_STEP(1)
+        FDF_SWEEP_STEP(2)
+        FDF_SWEEP_STEP(3)
+        FDF_SWEEP_STEP(4)
+        FDF_SWEEP_STEP(5)
+        FDF_SWEEP_STEP(6)
+        FDF_SWEEP_STEP(7)
     }
-#undef FDF_SWEEP_PAIR
-#undef FDF_SWEEP_DRAIN
-#undef FDF_SWEEP_B
-#undef FDF_SWEEP_A
-    // the last block ends on an odd step: at most its row is still queued, and the rings
-    // still hold the rows it needs (the score rows stop at p1 - 1)
-    if (u.pcount > 0 && !(u.flags & kFlagNoFullTest))
-        sweep_test<NMS, N, LC, ScoreT>(sh, u, lk, sh.pq, u.pcount);
-    u.pcount = 0;
-    if constexpr (NMS != kNmsOff) sweep_finalize<LC, ScoreT>(sh, u, p1 - 2, first_unfinal);
+#undef FDF_SWEEP_STEP
+    flush_tests<NMS, N, LC, ScoreT>(sh, u, lk, inflight, batch);
+    if constexpr (NMS != kNmsOff) finalize_upto<LC, ScoreT>(sh, u, first_unfinal, p1 - 2);
 }
 
 // Occupancy target: 4 workgroups (16 waves) per CU, registers <= 128 VGPRs.
@@ -443,7 +483,8 @@ void fast_sweep_kernel(BandParams P) {
     const uint32_t lane = tid & 63;
     const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
 
-    // XCD-aware static task mapping (see fast_band_kernel)
+    // XCD-aware static task mapping: consecutive bands of a frame land on one XCD (its L2
+    // then serves the halo rows two neighbouring bands share)
     const uint32_t b = blockIdx.x;
     const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
     const uint32_t task = k8 * q8 + min(k8, r8) + (b >> 3);
@@ -465,7 +506,6 @@ void fast_sweep_kernel(BandParams P) {
 
     uint8_t* wbase = smem_raw + wave * L.wave_bytes;
     SweepShared sh;
-    sh.data = wbase + L.data;
     sh.pq = reinterpret_cast<uint32_t*>(wbase + L.pq);
     sh.ring = wbase + L.ring;
     sh.kp = reinterpret_cast<uint32_t*>(wbase + L.kp);
@@ -507,11 +547,9 @@ void fast_sweep_kernel(BandParams P) {
             u.r0 = (int)(y0 + sub * sub_rows);
             u.r1 = (int)min(y0 + (sub + 1) * sub_rows, y0 + rows);
             if (u.r0 >= u.r1) continue;
-            // rows the sweep loads: up to r1 + ringr + 3 rounded to the 8-step block + 8 ahead
+            // rows the sweep loads: up to r1 + ringr + 2
             const int ringr = NMS == kNmsOff ? 0 : 1;
-            const int ys = u.r0 - ringr - 3;
-            const int steps = (u.r1 + ringr - ys + 7) & ~7;
-            if (last_frame && ys + steps + 2 + kSweepPrefetch >= u.src.tail_row) {
+            if (last_frame && u.r1 + ringr + 2 >= u.src.tail_row) {
                 u.src.rs = rs_exact;
                 sweep_unit<NMS, N, true>(sh, u, lk);
             } else {
@@ -522,7 +560,7 @@ void fast_sweep_kernel(BandParams P) {
     }
     __syncthreads();
 
-    // ---- count keep-bits and write the band slot (as fast_band_kernel)
+    // ---- count keep-bits and write the band slot
     const uint32_t nwords = rows * nw;
     const uint32_t per = (nwords + kThreads - 1) / kThreads;
     const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);

@@ -99,6 +99,61 @@ def detector(img, config):
     return [Point(int(x), int(y)) for x, y in detect_array(img, config)]
 
 
+def detect_rgb_array(rgb, config, device=0):
+    """Keypoints of an RGB8 (H, W, 3) image: converted on the device as image 0.24.6's
+    to_luma8 (what the reference's callers do, src/main.rs:58), then detected."""
+    arr = np.asarray(rgb)
+    if arr.ndim != 3 or arr.shape[2] != 3 or arr.dtype != np.uint8:
+        raise ValueError("expected an (H, W, 3) uint8 RGB image")
+    if arr.strides[1] != 3 or arr.strides[2] != 1:
+        arr = np.ascontiguousarray(arr)
+    cfg = _to_c_config(config)
+    h, w = arr.shape[:2]
+    ctx = context(device)
+    lib = _native.load()
+    n = ctypes.c_size_t(0)
+    stride = arr.strides[0] if arr.size else 3 * w
+    ptr = arr.ctypes.data if arr.size else None
+    rc = lib.fdf_detect_rgb(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), None, 0,
+                            ctypes.byref(n))
+    if rc == _native.FDF_ERR_CAPACITY:
+        out = np.empty((n.value, 2), dtype=np.uint32)
+        rc = lib.fdf_detect_rgb(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg),
+                                out.ctypes.data, out.shape[0], ctypes.byref(n))
+        check(rc, "fdf_detect_rgb")
+        return out[: n.value]
+    check(rc, "fdf_detect_rgb")
+    return np.empty((0, 2), dtype=np.uint32)
+
+
+def detector_rgb(rgb, config):
+    """``list[Point]`` for an RGB8 image (luma conversion on the device)."""
+    return [Point(int(x), int(y)) for x, y in detect_rgb_array(rgb, config)]
+
+
+def rgb_to_luma(frames, out, stream=None, device=None):
+    """Device-side RGB8 -> grey of torch uint8 CUDA tensors: ``frames`` (F, H, W, 3)
+    contiguous, ``out`` (F, H, W).  Asynchronous on ``stream`` (default: torch's current)."""
+    import torch
+
+    if frames.dim() != 4 or frames.shape[3] != 3 or frames.dtype != torch.uint8 or \
+            not frames.is_contiguous():
+        raise ValueError("frames must be a contiguous (F, H, W, 3) uint8 tensor")
+    if out.shape != frames.shape[:3] or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (F, H, W) uint8 tensor")
+    if not frames.is_cuda or not out.is_cuda:
+        raise ValueError("rgb_to_luma needs CUDA (HIP) tensors")
+    dev = frames.device.index if device is None else device
+    ctx = context(dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(frames.device)
+    f, h, w = frames.shape[:3]
+    lib = _native.load()
+    check(lib.fdf_rgb_to_luma_device(ctx.handle, frames.data_ptr(), f, w, h, 3 * w * h,
+                                     out.data_ptr(), ctypes.c_void_p(stream.cuda_stream)),
+          "fdf_rgb_to_luma_device")
+
+
 def detector_batch(frames, config, device=0):
     """Detect on a (F, H, W) uint8 stack.  Returns (points (K, 2) uint32, offsets (F+1,))
     where frame f's keypoints are points[offsets[f]:offsets[f+1]]."""

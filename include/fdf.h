@@ -103,6 +103,26 @@ int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t heigh
                size_t* n_out);
 
 /*
+ * RGB variant of fdf_detect: `data` holds RGB8 pixels (rows of 3 * width bytes at
+ * `stride_bytes`), converted on the device exactly as image 0.24.6's to_luma8 -- the
+ * reference's callers run `DynamicImage::ImageRgb8(img).to_luma8()` before detect
+ * (src/main.rs:58, tests/compare.rs:33) -- then detected as fdf_detect does.
+ */
+int fdf_detect_rgb(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+                   size_t stride_bytes, const fdf_config* cfg, fdf_point* out, size_t cap,
+                   size_t* n_out);
+
+/*
+ * Device-side RGB8 -> grey (image 0.24.6 to_luma8: (2126 r + 7152 g + 722 b) / 10000).
+ * `n_frames` frames of width x height RGB pixels (rows packed, 3 * width bytes) at
+ * d_rgb + f * rgb_frame_stride_bytes; grey frames packed (width * height bytes each) at
+ * d_grey.  Asynchronous on `stream` (NULL = the HIP null stream).  n_frames <= 65535.
+ */
+int fdf_rgb_to_luma_device(fdf_ctx* ctx, const uint8_t* d_rgb, uint32_t n_frames,
+                           uint32_t width, uint32_t height, uint64_t rgb_frame_stride_bytes,
+                           uint8_t* d_grey, void* stream);
+
+/*
  * Batched host variant: `n_frames` frames of width x height, frame f at
  * data + f * frame_stride_bytes (rows packed, stride == width).  Output is every frame's
  * list concatenated in frame order; frame f's points are out[frame_offsets[f] ..

@@ -166,3 +166,18 @@ int64_t fdf_oracle_detect(const uint8_t* img, uint32_t w, uint32_t h, size_t str
     free(score);
     return count;
 }
+
+/* image 0.24.6 color.rs rgb_to_luma for u8 (its Larger type is u32): the crate is not
+ * vendored in the reference, so this restates its published integer formula,
+ *   SRGB_LUMA = [2126, 7152, 722], SRGB_LUMA_DIV = 10000, l / SRGB_LUMA_DIV (truncating).
+ * Grey input (r = g = b) maps to itself; colour input is parity-unpinned. */
+void fdf_oracle_rgb_to_luma(const uint8_t* rgb, uint32_t w, uint32_t h, size_t rgb_stride,
+                            uint8_t* out) {
+    for (uint32_t y = 0; y < h; ++y) {
+        const uint8_t* row = rgb + (size_t)y * rgb_stride;
+        for (uint32_t x = 0; x < w; ++x) {
+            const uint32_t l = 2126u * row[3 * x] + 7152u * row[3 * x + 1] + 722u * row[3 * x + 2];
+            out[(size_t)y * w + x] = (uint8_t)(l / 10000u);
+        }
+    }
+}

@@ -20,6 +20,11 @@ int fdf_oracle_is_corner(uint8_t center, const uint8_t circle[16], uint8_t t, ui
 uint16_t fdf_oracle_score_max_threshold(uint8_t center, const uint8_t circle[16], uint8_t n);
 uint16_t fdf_oracle_score_sum_abs(uint8_t center, const uint8_t circle[16], uint8_t t);
 int fdf_oracle_check(uint32_t w, uint32_t h, uint8_t n, uint8_t nms, int* empty);
+/* image 0.24.6 DynamicImage::to_luma8 on Rgb<u8> (src/main.rs:58, tests/compare.rs:33):
+ * luma = (2126 r + 7152 g + 722 b) / 10000, integer division.  Rows of 3*w bytes at
+ * rgb_stride; output packed w*h. */
+void fdf_oracle_rgb_to_luma(const uint8_t* rgb, uint32_t w, uint32_t h, size_t rgb_stride,
+                            uint8_t* out);
 
 /* Returns the keypoint count (>= 0; only the first `cap` are written as x,y pairs into
  * out_xy and, if non-NULL, their NMS scores into out_scores) or a negative error code. */

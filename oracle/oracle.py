@@ -44,6 +44,9 @@ def _load():
         lib.fdf_oracle_check.restype = ctypes.c_int
         lib.fdf_oracle_check.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u8, u8,
                                          ctypes.POINTER(ctypes.c_int)]
+        lib.fdf_oracle_rgb_to_luma.restype = None
+        lib.fdf_oracle_rgb_to_luma.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_size_t, ctypes.c_void_p]
         lib.fdf_oracle_detect.restype = ctypes.c_int64
         lib.fdf_oracle_detect.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_size_t, u8, u8, u8, ctypes.c_void_p,
@@ -84,6 +87,18 @@ def score_max_threshold(center, circle, n):
 
 def score_sum_abs(center, circle, t):
     return int(_load().fdf_oracle_score_sum_abs(center, _circle_buf(circle), t))
+
+
+def rgb_to_luma(rgb):
+    """image 0.24.6 to_luma8 restated (fast_oracle.c): (H, W, 3) uint8 -> (H, W) uint8."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    if rgb.ndim != 3 or rgb.shape[2] != 3:
+        raise ValueError("(H, W, 3) image expected")
+    h, w = rgb.shape[:2]
+    out = np.empty((h, w), dtype=np.uint8)
+    if out.size:
+        _load().fdf_oracle_rgb_to_luma(rgb.ctypes.data, w, h, 3 * w, out.ctypes.data)
+    return out
 
 
 def check(w, h, n, nms):

@@ -268,3 +268,75 @@ def test_lane_segment_test_matches_oracle():
         bright = [p > c + t for p in ring]
         dark = [p < c - t for p in ring]
         assert b == _consecutive(bright, n) and d == _consecutive(dark, n), (c, t, n, ring)
+
+
+def _perm(hi, lo, sel):
+    """v_perm_b32: byte k of the result = byte sel_k of {hi:lo} (0-3 lo, 4-7 hi), 0x0c -> 0."""
+    src = [(lo >> (8 * i)) & 0xff for i in range(4)] + [(hi >> (8 * i)) & 0xff for i in range(4)]
+    out = 0
+    for k in range(4):
+        s = (sel >> (8 * k)) & 0xff
+        out |= (src[s] if s < 8 else 0) << (8 * k)
+    return out
+
+
+def test_sweep_gather_windows_pack_the_circle():
+    """fdf_sweep.hip issue_batch + pack_ring: 7 row windows (4 B from x-1 at y+-3, 8 B from
+    x-2 at y+-2, 8 B from x-3 at y-1..y+1) permuted into the 4 compare words, byte j of
+    word m = circle pixel 4j + m, and the centre."""
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, (20, 24), dtype=np.uint8)
+    flat = img.reshape(-1).astype(np.int64)
+    W = img.shape[1]
+
+    def word(o):
+        return int(sum(int(flat[o + i]) << (8 * i) for i in range(4)))
+
+    for y in range(3, 17):
+        for x in range(3, 21):
+            o = (y - 3) * W + x
+            a0, a6 = word(o - 1), word(o - 1 + 6 * W)
+            a1 = (word(o - 2 + W), word(o - 2 + W + 4))
+            a2 = (word(o - 3 + 2 * W), word(o - 3 + 2 * W + 4))
+            a3 = (word(o - 3 + 3 * W), word(o - 3 + 3 * W + 4))
+            a4 = (word(o - 3 + 4 * W), word(o - 3 + 4 * W + 4))
+            a5 = (word(o - 2 + 5 * W), word(o - 2 + 5 * W + 4))
+            w = [_perm(a3[1], a0, 0x0c0c0601) | _perm(a3[0], a6, 0x04010c0c),
+                 _perm(a4[1], a0, 0x0c0c0602) | _perm(a2[0], a6, 0x04000c0c),
+                 _perm(a1[1], a1[0], 0x000c0c04) | _perm(a5[1], a5[0], 0x0c00040c),
+                 _perm(a6, a2[1], 0x0c0c0602) | _perm(a0, a4[0], 0x04000c0c)]
+            for i, (dx, dy) in enumerate(CIRCLE):
+                assert (w[i & 3] >> (8 * (i >> 2))) & 0xff == img[y + dy, x + dx], (x, y, i)
+            assert a3[0] >> 24 == img[y, x]
+
+
+def test_luma_restatement():
+    """fdf_oracle_rgb_to_luma == image 0.24.6's integer formula; identity on grey pixels
+    (the reference's media image is grey, r = g = b, so its detections are pinned)."""
+    rng = np.random.default_rng(3)
+    rgb = rng.integers(0, 256, (17, 23, 3), dtype=np.uint8)
+    r, g, b = (rgb[..., k].astype(np.uint32) for k in range(3))
+    want = ((2126 * r + 7152 * g + 722 * b) // 10000).astype(np.uint8)
+    assert np.array_equal(oracle.rgb_to_luma(rgb), want)
+    v = np.arange(256, dtype=np.uint8)
+    assert np.array_equal(oracle.rgb_to_luma(np.stack([v, v, v], -1)[None]), v[None])
+
+
+def test_cli_helpers_without_gpu(tmp_path):
+    """cli.py host helpers: the overlay luma equals the restated formula, keypoint pixels go
+    red except at x <= 0 / y <= 0 (draw_plus_sized), and the .txt format is "x y" lines."""
+    from feature_detector_fast_amd import cli
+
+    rng = np.random.default_rng(4)
+    rgb = rng.integers(0, 256, (9, 11, 3), dtype=np.uint8)
+    assert np.array_equal(cli.luma8(rgb), oracle.rgb_to_luma(rgb))
+    grey = oracle.rgb_to_luma(rgb)
+    pts = np.array([[3, 4], [0, 5], [10, 8]], dtype=np.uint32)
+    ov = cli.overlay(grey, pts)
+    assert tuple(ov[4, 3]) == (255, 0, 0) and tuple(ov[8, 10]) == (255, 0, 0)
+    assert tuple(ov[5, 0]) == (grey[5, 0],) * 3
+    f = tmp_path / "k.txt"
+    cli.write_keypoints(pts, str(f))
+    assert f.read_text() == "3 4\n0 5\n10 8\n"
+    assert np.array_equal(workloads.read_points(str(f)), pts)
+    assert cli.main(["--help"]) == 0
