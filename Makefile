@@ -11,7 +11,7 @@ ARCH ?= gfx950
 PKG := feature_detector_fast_amd
 CSRC := $(PKG)/csrc
 LIBFDF := $(PKG)/libfdf.so
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude $(EXTRA_HIPFLAGS)
 
 all: $(LIBFDF) oracle/liboracle.so oracle/libfast_avx2.so tests/cpp/test_cpp_api
 

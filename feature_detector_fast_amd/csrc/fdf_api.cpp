@@ -103,9 +103,9 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score
     if (const char* e = std::getenv("FDF_NSUB")) g.nsub = (uint32_t)std::strtoul(e, nullptr, 0);
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
-    // LDS per workgroup sets the workgroups per CU: 4 without NMS, 3 for max-threshold's
-    // 16-row score ring, 2 for SAD's 16-bit one (tools/ablate.py sweeps).
-    uint32_t budget = score_bytes == 0 ? 40000 : (score_bytes == 1 ? 53000 : 80000);
+    // LDS per workgroup sets the workgroups per CU: 4 without NMS and for max-threshold,
+    // 3 for SAD's 16-bit score ring (tools/ablate.py sweeps).
+    uint32_t budget = score_bytes == 2 ? 53000 : 40000;
     if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the

@@ -28,7 +28,19 @@ constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, nev
 __host__ __device__ constexpr int lane_cols_for(uint32_t nms) { return nms == 0 ? 16 : 8; }
 __host__ __device__ constexpr int strip_cols(int lc) { return 62 * lc; }
 constexpr int kSweepPixelQ = 256;             // candidate pixel FIFO per wave (power of two)
-constexpr int kSweepRing = 16;                // NMS score ring rows per wave (power of two)
+// NMS score ring rows per wave (power of two): deep enough that testing can lag the sweep
+// while a 64-pixel batch fills; SAD's 16-bit scores make its ring twice as big per row.
+// (8 rows measured faster than 16: the smaller ring buys a workgroup per CU, and batches
+// are issued partially full once their oldest pixel would outrun it.)
+#ifndef FDF_RING_MAXT
+#define FDF_RING_MAXT 8
+#endif
+#ifndef FDF_RING_SAD
+#define FDF_RING_SAD 8
+#endif
+__host__ __device__ constexpr int sweep_ring_rows(uint32_t nms) {
+    return nms == 0 ? 0 : (nms == 1 ? FDF_RING_MAXT : FDF_RING_SAD);
+}
 constexpr int kSweepKpCap = 256;              // unfinalized NMS keypoints per wave
 constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per workgroup)
 
@@ -47,7 +59,7 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     SweepLayout L;
     uint32_t o = 0;
     L.pq = o;       o += kSweepPixelQ * 4;
-    L.ring = o;     o += kSweepRing * 64 * lc * score_bytes;
+    L.ring = o;     o += sweep_ring_rows(score_bytes) * 64 * lc * score_bytes;
     L.kp = o;       o += score_bytes ? kSweepKpCap * 4 : 0;
     L.wave_bytes = align16(o);
     L.bitmap = 4 * L.wave_bytes;

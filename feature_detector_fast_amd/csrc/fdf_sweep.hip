@@ -99,7 +99,7 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
 
 struct SweepShared {
     uint32_t* pq;          // kSweepPixelQ FIFO of (row << 10) | strip column
-    void* ring;            // kSweepRing x 64*LC scores (NMS), row y in slot y & 15
+    void* ring;            // sweep_ring_rows x 64*LC scores (NMS), row y in slot y % rows
     uint32_t* kp;          // kSweepKpCap: (row << 10) | strip column
     uint32_t* bitmap;      // band keep-bits, R x words_per_row
 };
@@ -119,7 +119,8 @@ struct UnitCtx {
 
 template <int LC, typename ScoreT>
 __device__ __forceinline__ ScoreT* ring_at(const SweepShared& sh, int y, int cl) {
-    return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kSweepRing - 1)) * (64 * LC) + cl;
+    constexpr int kRing = sweep_ring_rows(sizeof(ScoreT));   // score bytes 1 / 2 = nms 1 / 2
+    return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kRing - 1)) * (64 * LC) + cl;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -321,6 +322,11 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     constexpr int LC = lane_cols_for(NMS);
     constexpr int M = LC / 4;
     constexpr int kIssue = sweep_issue_every(NMS);
+    // the oldest queued row may lag the sweep by this much before a partial batch is issued
+    // (the ring keeps rows >= (oldest untested) - 2 up to the current row)
+    constexpr int kLagLimit = NMS == kNmsOff ? 1 << 30
+                                             : (sweep_ring_rows(NMS) - kIssue - 3 > 1
+                                                    ? sweep_ring_rows(NMS) - kIssue - 3 : 1);
     using RowV = typename LaneRow<LC>::type;
     const uint32_t lane = u.lane;
     const int H = (int)u.src.H, W = (int)u.src.W;
@@ -401,7 +407,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             if (live) {                                                                      \
                 /* the ring slot of row yv still holds row yv - 16: if that row is still */  \
                 /* needed as an NMS neighbour, catch testing and NMS up first */             \
-                if (yv - kSweepRing >= first_unfinal - 1) {                                  \
+                if (yv - sweep_ring_rows(NMS) >= first_unfinal - 1) {                        \
                     flush_tests<NMS, N, LC, ScoreT>(sh, u, lk, inflight, batch);             \
                     finalize_upto<LC, ScoreT>(sh, u, first_unfinal, yv - 2);                 \
                 }                                                                            \
@@ -437,9 +443,15 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, batch);                        \
                 inflight = false;                                                            \
             }                                                                                \
-            const bool full = u.tail - u.head >= 64;                                         \
-            if (full && (u.flags & kFlagNoFullTest)) u.head += 64;                           \
-            const uint32_t n = (full && !(u.flags & kFlagNoFullTest)) ? 64u : 0u;            \
+            const uint32_t pend = u.tail - u.head;                                           \
+            bool go = pend >= 64;                                                            \
+            if constexpr (NMS != kNmsOff) {                                                  \
+                /* a partial batch goes too once its oldest pixel would outrun the ring */   \
+                if (!go && pend > 0)                                                         \
+                    go = yv - (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 10) >= kLagLimit;  \
+            }                                                                                \
+            if (go && (u.flags & kFlagNoFullTest)) u.head += min(pend, 64u);                 \
+            const uint32_t n = (go && !(u.flags & kFlagNoFullTest)) ? min(pend, 64u) : 0u;   \
             batch = issue_batch<LC>(sh, u, n);                                               \
             inflight = n != 0;                                                               \
             if constexpr (NMS != kNmsOff) {                                                  \
