@@ -64,8 +64,6 @@ struct RowSource {
     int tail_row;                // EXACT: rows >= tail_row may have windows crossing W * H
 };
 
-constexpr int kOutOfRange = 0x7ffffff0;   // a buffer offset past any frame: loads return 0
-
 // Bytes [xb, xb+LC) of image row y: one LC-byte buffer load at any byte offset (gfx950
 // buffer loads need no alignment).  No branch, so the row prefetch stays a plain stream the
 // compiler's vmcnt bookkeeping can count.  Rows outside the frame and negative offsets read
@@ -78,9 +76,12 @@ template <int LC, bool EXACT>
 __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& src, int y,
                                                               int xb) {
     using RowV = typename LaneRow<LC>::type;
-    const int off = y * (int)src.W + xb;
-    const bool in = y >= 0 && y < (int)src.H && y <= src.ylast && off >= 0;
-    const int o = in ? off : kOutOfRange;
+    // y is wave-uniform, so the row test is scalar: a row outside [0, H) or past the unit's
+    // last row gets an offset of 2^31 + xb, past any frame.  One VALU add per load; a
+    // negative xb in row 0 wraps to >= 2^32 - LC, also out of range (reads 0).
+    const bool in = y >= 0 && y < (int)src.H && y <= src.ylast;
+    const uint32_t rowoff = in ? (uint32_t)(y * (int)src.W) : 0x80000000u;
+    const int o = (int)(rowoff + (uint32_t)xb);
     if constexpr (EXACT) {
         if (y >= src.tail_row) {   // wave-uniform
             RowV r = (RowV)(0u);
@@ -98,7 +99,7 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
 }
 
 struct SweepShared {
-    uint32_t* pq;          // kSweepPixelQ FIFO of (row << 10) | strip column
+    uint32_t* pq;          // kSweepPixelQ FIFO of (row << 11) | (lane << 5) | flag bit
     void* ring;            // sweep_ring_rows x 64*LC scores (NMS), row y in slot y % rows
     uint32_t* kp;          // kSweepKpCap: (row << 10) | strip column
     uint32_t* bitmap;      // band keep-bits, R x words_per_row
@@ -143,7 +144,11 @@ template <int LC>
 __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, uint32_t n) {
     Batch b;
     b.act = u.lane < n;
-    b.code = b.act ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
+    // FIFO entry (row << 11) | (lane << 5) | bit, bit 8j + m = lane column 4m + j  ->
+    // the test's code (row << 10) | strip column
+    const uint32_t e = b.act ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
+    const uint32_t bit = e & 31u;
+    b.code = ((e >> 11) << 10) | (((e >> 5) & 63u) * LC + 4 * (bit & 7u) + (bit >> 3));
     u.head += n;
     const int W = (int)u.src.W;
     // inactive lanes read around centre (3, 3), which every tested frame has
@@ -333,19 +338,18 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     const int xb = u.S - LC + LC * (int)lane;
     // candidate columns of this lane: owned centres, plus for NMS the two border columns the
     // strip's edge keypoints compare against (scores only)
-    RowV vmask;
+    // (bit 8j + m = lane column 4m + j, the order the candidate mask is built in)
+    uint32_t vmask = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-        uint32_t v = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int x = xb + 4 * m + j;
             bool ok = x >= 3 && x < W - 3;
             if (lane == 0) ok = ok && NMS != kNmsOff && x == u.S - 1;
             if (lane == 63) ok = ok && NMS != kNmsOff && x == u.S + strip_cols(LC);
-            if (ok) v |= 0x80u << (8 * j);
+            if (ok) vmask |= 1u << (8 * j + m);
         }
-        vmask[m] = v;
     }
     const int ringr = NMS == kNmsOff ? 0 : 1;
     const int p0 = u.r0 - ringr, p1 = u.r1 + ringr;   // rows run through the pre-filter
@@ -400,7 +404,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                     br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
                     nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
                 }                                                                            \
-                cand[m] = (br | ~nd) & vmask[m];                                             \
+                cand[m] = br | ~nd;                                                          \
             }                                                                                \
         }                                                                                    \
         if constexpr (NMS != kNmsOff) {                                                      \
@@ -416,18 +420,18 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             }                                                                                \
         }                                                                                    \
         /* candidate pixels into the FIFO, one per lane per round: column 4m + j of the */   \
-        /* lane is bit 8j + m of cm */                                                       \
+        /* lane is bit 8j + m of cm; the entry keeps the bit, issue_batch decodes it */      \
+        const uint32_t code_base = ((uint32_t)yv << 11) | (lane << 5);                       \
         uint32_t cm = 0;                                                                     \
-        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= cand[m] >> (7 - m);              \
+        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= (cand[m] >> (7 - m)) & (0x01010101u << m); \
+        cm &= vmask;                                                                         \
         for (;;) {                                                                           \
             const bool has = cm != 0;                                                        \
             const uint64_t bal = wave_ballot(has);                                           \
             if (bal == 0) break;                                                             \
             if (has) {                                                                       \
-                const uint32_t bit = (uint32_t)__builtin_ctz(cm);                            \
-                const uint32_t col = 4 * (bit & 7u) + (bit >> 3);                            \
                 sh.pq[(u.tail + lanes_below(bal)) & (kSweepPixelQ - 1)] =                    \
-                    ((uint32_t)yv << 10) | (LC * lane + col);                                \
+                    code_base | (uint32_t)__builtin_ctz(cm);                                 \
                 cm &= cm - 1;                                                                \
             }                                                                                \
             u.tail += (uint32_t)__popcll(bal);                                               \
@@ -448,7 +452,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             if constexpr (NMS != kNmsOff) {                                                  \
                 /* a partial batch goes too once its oldest pixel would outrun the ring */   \
                 if (!go && pend > 0)                                                         \
-                    go = yv - (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 10) >= kLagLimit;  \
+                    go = yv - (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 11) >= kLagLimit;  \
             }                                                                                \
             if (go && (u.flags & kFlagNoFullTest)) u.head += min(pend, 64u);                 \
             const uint32_t n = (go && !(u.flags & kFlagNoFullTest)) ? min(pend, 64u) : 0u;   \
@@ -457,7 +461,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             if constexpr (NMS != kNmsOff) {                                                  \
                 /* rows before the oldest untested candidate are fully tested */             \
                 int r = yv + 1;                                                              \
-                if (u.tail != u.head) r = (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 10);   \
+                if (u.tail != u.head) r = (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 11);   \
                 if (inflight) r = min(r, (int)(__builtin_amdgcn_readfirstlane(batch.code) >> 10)); \
                 finalize_upto<LC, ScoreT>(sh, u, first_unfinal, r - 2);                      \
             }                                                                                \
