@@ -23,20 +23,24 @@ constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compa
 constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
 
 // Column-sweep kernel (fdf_sweep.hip): per-wave LDS region + the band bitmap.
-// Columns per lane: 16 without NMS; 8 with NMS, whose per-wave score ring would otherwise
-// cut the waves per CU.  A strip is 62 lanes wide (lanes 0 and 63 are halo lanes).
-__host__ __device__ constexpr int lane_cols_for(uint32_t nms) { return nms == 0 ? 16 : 8; }
+// Columns per lane (16; FDF_LC_NMS = 8 halves the NMS score ring for A/B runs).  A strip is
+// 62 lanes wide (lanes 0 and 63 are halo lanes).
+#ifndef FDF_LC_NMS
+#define FDF_LC_NMS 16
+#endif
+__host__ __device__ constexpr int lane_cols_for(uint32_t nms) { return nms == 0 ? 16 : FDF_LC_NMS; }
 __host__ __device__ constexpr int strip_cols(int lc) { return 62 * lc; }
 constexpr int kSweepPixelQ = 256;             // candidate pixel FIFO per wave (power of two)
 // NMS score ring rows per wave (power of two): deep enough that testing can lag the sweep
 // while a 64-pixel batch fills; SAD's 16-bit scores make its ring twice as big per row.
-// (8 rows measured faster than 16: the smaller ring buys a workgroup per CU, and batches
-// are issued partially full once their oldest pixel would outrun it.)
+// (4 rows of 16-column lanes measured fastest: 8 or 16 rows, or 8-column lanes, cost a
+// workgroup per CU; batches are issued partially full once their oldest pixel would
+// outrun the ring.  tools/build_variant.sh rebuilds with other values for A/B runs.)
 #ifndef FDF_RING_MAXT
-#define FDF_RING_MAXT 8
+#define FDF_RING_MAXT 4
 #endif
 #ifndef FDF_RING_SAD
-#define FDF_RING_SAD 8
+#define FDF_RING_SAD 4
 #endif
 __host__ __device__ constexpr int sweep_ring_rows(uint32_t nms) {
     return nms == 0 ? 0 : (nms == 1 ? FDF_RING_MAXT : FDF_RING_SAD);
@@ -46,7 +50,10 @@ constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per work
 
 // A full-test batch is issued every kSweepIssue(nms) rows once 64 candidates are queued and
 // is evaluated the same number of rows later.
-__host__ __device__ constexpr int sweep_issue_every(uint32_t nms) { return nms == 0 ? 2 : 4; }
+#ifndef FDF_ISSUE_NMS
+#define FDF_ISSUE_NMS 4
+#endif
+__host__ __device__ constexpr int sweep_issue_every(uint32_t nms) { return nms == 0 ? 2 : FDF_ISSUE_NMS; }
 
 struct SweepLayout {
     uint32_t pq, ring, kp, wave_bytes, bitmap, total;
