@@ -24,7 +24,10 @@ $(CSRC)/fdf_sweep.o: $(CSRC)/fdf_sweep.hip $(CSRC)/fdf_kernels.h $(CSRC)/fdf_com
 $(CSRC)/fdf_api.o: $(CSRC)/fdf_api.cpp $(CSRC)/fdf_kernels.h include/fdf.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_api.o
+$(CSRC)/fdf_pipeline.o: $(CSRC)/fdf_pipeline.cpp include/fdf.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_api.o $(CSRC)/fdf_pipeline.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle/liboracle.so: oracle/fast_oracle.c oracle/fast_oracle.h

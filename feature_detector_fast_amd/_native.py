@@ -22,13 +22,21 @@ FDF_ERR_NMS = 4
 FDF_ERR_DEVICE = 5
 FDF_ERR_ARG = 6
 FDF_ERR_ALLOC = 7
+FDF_ERR_BUSY = 8
+FDF_ERR_DROPPED = 9
+# enum fdf_pipe_flags
+FDF_PIPE_RGB = 1
+FDF_PIPE_SCORES = 2
 
 # Every symbol include/fdf.h declares (tests/test_abi.py checks the .so exports them all).
 EXPORTED_SYMBOLS = (
     "fdf_abi_version", "fdf_status_string", "fdf_device_count", "fdf_validate",
     "fdf_ctx_create", "fdf_ctx_destroy", "fdf_ctx_stream", "fdf_ctx_set_timing",
     "fdf_ctx_timing", "fdf_detect", "fdf_detect_rgb", "fdf_rgb_to_luma_device",
-    "fdf_detect_batch", "fdf_detect_device", "fdf_score_points",
+    "fdf_detect_batch", "fdf_detect_device", "fdf_score_points", "fdf_detect_scored",
+    "fdf_detect_batch_scored", "fdf_score_device", "fdf_pipeline_create",
+    "fdf_pipeline_destroy", "fdf_pipeline_acquire", "fdf_pipeline_submit", "fdf_pipeline_push",
+    "fdf_pipeline_collect",
 )
 
 
@@ -115,6 +123,26 @@ def load():
     lib.fdf_detect_device.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp]
     lib.fdf_score_points.restype = ctypes.c_int
     lib.fdf_score_points.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, vp]
+    lib.fdf_detect_scored.restype = ctypes.c_int
+    lib.fdf_detect_scored.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, vp, sz, ctypes.POINTER(sz)]
+    lib.fdf_detect_batch_scored.restype = ctypes.c_int
+    lib.fdf_detect_batch_scored.argtypes = [vp, vp, u32, u32, u32, sz, cfgp, vp, vp, sz, vp,
+                                            ctypes.POINTER(sz)]
+    lib.fdf_score_device.restype = ctypes.c_int
+    lib.fdf_score_device.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp, vp]
+    lib.fdf_pipeline_create.restype = ctypes.c_int
+    lib.fdf_pipeline_create.argtypes = [ctypes.c_int, u32, u32, u32, u32, u64, u32, cfgp,
+                                        ctypes.POINTER(vp)]
+    lib.fdf_pipeline_destroy.restype = None
+    lib.fdf_pipeline_destroy.argtypes = [vp]
+    lib.fdf_pipeline_acquire.restype = ctypes.c_int
+    lib.fdf_pipeline_acquire.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
+    lib.fdf_pipeline_submit.restype = ctypes.c_int
+    lib.fdf_pipeline_submit.argtypes = [vp, u64, u32]
+    lib.fdf_pipeline_push.restype = ctypes.c_int
+    lib.fdf_pipeline_push.argtypes = [vp, vp, u32, sz, ctypes.POINTER(u64)]
+    lib.fdf_pipeline_collect.restype = ctypes.c_int
+    lib.fdf_pipeline_collect.argtypes = [vp, u64, vp, vp, sz, vp, ctypes.POINTER(sz)]
     del u8p
     _lib = lib
     return lib

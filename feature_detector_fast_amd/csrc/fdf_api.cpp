@@ -26,6 +26,7 @@ struct fdf_ctx {
     uint8_t* d_rgb = nullptr;           size_t rgb_bytes = 0;      // host-API RGB staging
     uint2* d_out = nullptr;             size_t out_points = 0;     // host-API output
     uint64_t* d_offsets = nullptr;      size_t offsets_n = 0;      // host-API frame offsets
+    uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
     unsigned long long* d_state = nullptr; size_t state_n = 0;     // compaction look-back
@@ -218,10 +219,21 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
 // Shared body of fdf_detect / fdf_detect_batch: host frames in, host points out.
 // `rgb`: the frames are RGB8 (rows of 3 * w bytes at row_stride), converted on the device
 // with image 0.24.6's to_luma8 before detection (src/main.rs:58).
+// The score reported with a keypoint: the NMS mode's own, max-threshold when NMS is off.
+uint32_t score_kind(uint32_t nms) {
+    return nms == FDF_NMS_SUM_ABSOLUTE ? FDF_NMS_SUM_ABSOLUTE : FDF_NMS_MAX_THRESHOLD;
+}
+// ~4 points per thread on average, 1..64 workgroups per frame.
+uint32_t score_blocks(uint64_t points, uint32_t n_frames) {
+    const uint64_t per_frame = points / std::max<uint32_t>(n_frames, 1u);
+    return (uint32_t)std::min<uint64_t>(64, per_frame / 1024 + 1);
+}
+
 int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
                 size_t row_stride, size_t frame_stride, const fdf_config* cfg, fdf_point* out,
-                size_t cap, uint64_t* frame_offsets, size_t* n_out, bool rgb = false) {
-    if (!ctx || !n_out || (cap && !out)) return FDF_ERR_ARG;
+                size_t cap, uint64_t* frame_offsets, size_t* n_out, bool rgb = false,
+                uint16_t* out_scores = nullptr, bool scored = false) {
+    if (!ctx || !n_out || (cap && !out) || (scored && cap && !out_scores)) return FDF_ERR_ARG;
     int rc = check_config(cfg);
     if (rc) return rc;
     int empty = 0;
@@ -276,6 +288,17 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
     if (offs != frame_offsets && offs != local) delete[] offs;
     if (e != hipSuccess) return FDF_ERR_DEVICE;
     const size_t ncopy = (size_t)std::min<uint64_t>(total, cap);
+    if (scored && ncopy) {
+        if ((rc = ensure(&ctx->d_scores, &ctx->scores_n, ncopy, false, ctx->stream))) return rc;
+        e = fdfk::launch_score_frames(ctx->d_in, w, frame_bytes, n_frames, ctx->d_out,
+                                      ctx->d_offsets, ncopy, score_blocks(ncopy, n_frames),
+                                      score_kind(cfg->nms), cfg->threshold, cfg->count,
+                                      ctx->d_scores, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_scores, ctx->d_scores, ncopy * sizeof(uint16_t),
+                               hipMemcpyDeviceToHost, ctx->stream);
+        if (e != hipSuccess) return FDF_ERR_DEVICE;
+    }
     if (ncopy) {
         e = hipMemcpyAsync(out, ctx->d_out, ncopy * sizeof(fdf_point), hipMemcpyDeviceToHost,
                            ctx->stream);
@@ -302,6 +325,8 @@ const char* fdf_status_string(int status) {
         case FDF_ERR_DEVICE: return "HIP device error";
         case FDF_ERR_ARG: return "invalid argument";
         case FDF_ERR_ALLOC: return "allocation failed";
+        case FDF_ERR_BUSY: return "pipeline slot still holds uncollected results";
+        case FDF_ERR_DROPPED: return "batch found more keypoints than the pipeline's device capacity";
         default: return "unknown status";
     }
 }
@@ -345,6 +370,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_rgb);
         (void)hipFree(ctx->d_out);
         (void)hipFree(ctx->d_offsets);
+        (void)hipFree(ctx->d_scores);
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_state);
@@ -412,6 +438,48 @@ int fdf_rgb_to_luma_device(fdf_ctx* ctx, const uint8_t* d_rgb, uint32_t n_frames
                                  reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
         return FDF_ERR_DEVICE;
     return FDF_OK;
+}
+
+int fdf_detect_scored(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+                      size_t stride_bytes, const fdf_config* cfg, fdf_point* out,
+                      uint16_t* out_scores, size_t cap, size_t* n_out) {
+    return detect_host(ctx, data, 1, width, height, stride_bytes, 0, cfg, out, cap, nullptr,
+                       n_out, false, out_scores, true);
+}
+
+int fdf_detect_batch_scored(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames,
+                            uint32_t width, uint32_t height, size_t frame_stride_bytes,
+                            const fdf_config* cfg, fdf_point* out, uint16_t* out_scores,
+                            size_t cap, uint64_t* frame_offsets, size_t* n_out) {
+    if (n_frames > 1 && frame_stride_bytes < (size_t)width * height) return FDF_ERR_ARG;
+    if (n_frames > 65535u) return FDF_ERR_ARG;
+    return detect_host(ctx, data, n_frames, width, height, width, frame_stride_bytes, cfg, out,
+                       cap, frame_offsets, n_out, false, out_scores, true);
+}
+
+int fdf_score_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
+                     uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
+                     const fdf_config* cfg, const fdf_point* d_points, uint64_t cap,
+                     const uint64_t* d_frame_offsets, uint16_t* d_scores, void* stream) {
+    if (!ctx || !d_frame_offsets) return FDF_ERR_ARG;
+    int rc = check_config(cfg);
+    if (rc) return rc;
+    int empty = 0;
+    rc = check_shape(width, height, &empty);
+    if (rc) return rc;
+    if (empty || n_frames == 0 || cap == 0) return FDF_OK;
+    if (!d_frames || !d_points || !d_scores || n_frames > 65535u) return FDF_ERR_ARG;
+    if (n_frames > 1 && frame_stride_bytes < (uint64_t)width * height) return FDF_ERR_ARG;
+    DeviceGuard guard(ctx->device);
+    const uint64_t fs = n_frames > 1 ? frame_stride_bytes : (uint64_t)width * height;
+    const uint64_t est = std::min<uint64_t>(cap, (uint64_t)width * height / 32 * n_frames);
+    return fdfk::launch_score_frames(d_frames, width, fs, n_frames,
+                                     reinterpret_cast<const uint2*>(d_points), d_frame_offsets,
+                                     cap, score_blocks(est, n_frames), score_kind(cfg->nms),
+                                     cfg->threshold, cfg->count, d_scores,
+                                     reinterpret_cast<hipStream_t>(stream)) == hipSuccess
+               ? FDF_OK
+               : FDF_ERR_DEVICE;
 }
 
 int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t width,

@@ -134,5 +134,9 @@ hipError_t launch_rgb_to_luma(const uint8_t* rgb, uint32_t n_frames, uint32_t pi
 hipError_t launch_score_points(const uint8_t* img, uint32_t width, const uint2* pts,
                                uint32_t npts, uint32_t nms, uint32_t t, uint32_t n,
                                uint16_t* out, hipStream_t stream);
+hipError_t launch_score_frames(const uint8_t* frames, uint32_t width, uint64_t frame_stride,
+                               uint32_t n_frames, const uint2* pts, const uint64_t* offsets,
+                               uint64_t cap, uint32_t blocks_per_frame, uint32_t nms,
+                               uint32_t t, uint32_t n, uint16_t* out, hipStream_t stream);
 
 }  // namespace fdfk

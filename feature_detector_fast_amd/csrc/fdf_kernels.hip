@@ -187,20 +187,22 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
 // Point scoring (extension, fdf_score_points): literal formulas of the reference's score
 // functions, valid for any point, one thread per point.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void score_points_kernel(const uint8_t* img, uint32_t W,
-                                                           const uint2* pts, uint32_t npts,
-                                                           uint32_t nms, uint32_t t,
-                                                           uint32_t n, uint16_t* out) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= npts) return;
-    const uint2 pt = pts[k];
+__device__ __forceinline__ uint16_t score_point(const uint8_t* img, uint32_t W, uint2 pt,
+                                                uint32_t nms, uint32_t t, uint32_t n) {
     const int c = img[(uint64_t)pt.y * W + pt.x];
     int d[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
         d[i] = c - (int)img[(uint64_t)((int)pt.y + circle_dy(i)) * W + (int)pt.x + circle_dx(i)];
     uint32_t score;
-    if (nms == kNmsMaxThreshold) {   // src/fast_simd.rs:623-718
+    if (nms == kNmsSumAbsolute) {    // src/fast_simd.rs:722-749
+        uint32_t sb = 0, sd = 0;
+        for (int i = 0; i < 16; ++i) {
+            sb += (uint32_t)max(d[i] - (int)t, 0);
+            sd += (uint32_t)max(-d[i] - (int)t, 0);
+        }
+        score = max(sb, sd);
+    } else {                          // src/fast_simd.rs:623-718
         int hi = -32768, lo = 32767;
         for (int kk = 0; kk < 16; ++kk) {
             int mn = 32767, mx = -32768;
@@ -212,15 +214,35 @@ __global__ __launch_bounds__(256) void score_points_kernel(const uint8_t* img, u
             lo = min(lo, mx);
         }
         score = (uint32_t)min(abs(hi), abs(lo));
-    } else {                          // src/fast_simd.rs:722-749
-        uint32_t sb = 0, sd = 0;
-        for (int i = 0; i < 16; ++i) {
-            sb += (uint32_t)max(d[i] - (int)t, 0);
-            sd += (uint32_t)max(-d[i] - (int)t, 0);
-        }
-        score = max(sb, sd);
     }
-    out[k] = (uint16_t)score;
+    return (uint16_t)score;
+}
+
+__global__ __launch_bounds__(256) void score_points_kernel(const uint8_t* img, uint32_t W,
+                                                           const uint2* pts, uint32_t npts,
+                                                           uint32_t nms, uint32_t t,
+                                                           uint32_t n, uint16_t* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= npts) return;
+    out[k] = score_point(img, W, pts[k], nms, t, n);
+}
+
+// Batched form for detect output: frame f (blockIdx.y) scores points
+// [offsets[f], offsets[f+1]) against its own frame; offsets are read on the device, so the
+// launch needs no host round trip after detection.
+__global__ __launch_bounds__(256) void score_frames_kernel(const uint8_t* frames, uint32_t W,
+                                                           uint64_t frame_stride,
+                                                           const uint2* pts,
+                                                           const uint64_t* offsets,
+                                                           uint64_t cap, uint32_t nms,
+                                                           uint32_t t, uint32_t n,
+                                                           uint16_t* out) {
+    const uint32_t f = blockIdx.y;
+    const uint64_t b = offsets[f], e = min(offsets[f + 1], cap);
+    const uint8_t* img = frames + (uint64_t)f * frame_stride;
+    for (uint64_t k = b + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < e;
+         k += (uint64_t)gridDim.x * blockDim.x)
+        out[k] = score_point(img, W, pts[k], nms, t, n);
 }
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream) {
@@ -240,6 +262,16 @@ hipError_t launch_score_points(const uint8_t* img, uint32_t W, const uint2* pts,
     return hipGetLastError();
 }
 
+hipError_t launch_score_frames(const uint8_t* frames, uint32_t W, uint64_t frame_stride,
+                               uint32_t n_frames, const uint2* pts, const uint64_t* offsets,
+                               uint64_t cap, uint32_t blocks_per_frame, uint32_t nms,
+                               uint32_t t, uint32_t n, uint16_t* out, hipStream_t stream) {
+    if (n_frames == 0 || cap == 0) return hipSuccess;
+    if (n_frames > 65535u || blocks_per_frame == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(score_frames_kernel, dim3(blocks_per_frame, n_frames), dim3(256), 0,
+                       stream, frames, W, frame_stride, pts, offsets, cap, nms, t, n, out);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------------------
 // RGB8 -> grey: image 0.24.6 color.rs rgb_to_luma for u8 (not vendored in the reference;

@@ -224,6 +224,94 @@ def keypoint_scores(img, points, config, device=0):
     return scores
 
 
+def detect_scored_array(img, config, device=0):
+    """Keypoints with scores: ((K, 2) uint32 (x, y) in raster order, (K,) uint16 scores).
+    The score is the one the configured NMS suppresses with, max-threshold when NMS is off
+    (fdf_detect_scored)."""
+    arr = _as_pixels(img)
+    cfg = _to_c_config(config)
+    h, w = arr.shape
+    ctx = context(device)
+    lib = _native.load()
+    n = ctypes.c_size_t(0)
+    stride = arr.strides[0] if arr.size else w
+    ptr = arr.ctypes.data if arr.size else None
+    rc = lib.fdf_detect_scored(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), None, None, 0,
+                               ctypes.byref(n))
+    if rc == _native.FDF_ERR_CAPACITY:
+        out = np.empty((n.value, 2), dtype=np.uint32)
+        scores = np.empty(n.value, dtype=np.uint16)
+        rc = lib.fdf_detect_scored(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg),
+                                   out.ctypes.data, scores.ctypes.data, out.shape[0],
+                                   ctypes.byref(n))
+        check(rc, "fdf_detect_scored")
+        return out[: n.value], scores[: n.value]
+    check(rc, "fdf_detect_scored")
+    return np.empty((0, 2), dtype=np.uint32), np.empty(0, dtype=np.uint16)
+
+
+def detector_scored(img, config):
+    """``list[(Point, score)]`` in raster order (the (x, y, score) output)."""
+    pts, scores = detect_scored_array(img, config)
+    return [(Point(int(x), int(y)), int(s)) for (x, y), s in zip(pts, scores)]
+
+
+def detector_batch_scored(frames, config, device=0):
+    """detector_batch with scores: (points (K, 2), scores (K,) uint16, offsets (F+1,))."""
+    frames = np.ascontiguousarray(np.asarray(frames), dtype=np.uint8)
+    if frames.ndim != 3:
+        raise ValueError("expected a (F, H, W) uint8 stack")
+    f, h, w = frames.shape
+    cfg = _to_c_config(config)
+    ctx = context(device)
+    lib = _native.load()
+    offsets = np.zeros(f + 1, dtype=np.uint64)
+    n = ctypes.c_size_t(0)
+    ptr = frames.ctypes.data if frames.size else None
+    rc = lib.fdf_detect_batch_scored(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg), None,
+                                     None, 0, offsets.ctypes.data, ctypes.byref(n))
+    out = np.empty((0, 2), dtype=np.uint32)
+    scores = np.empty(0, dtype=np.uint16)
+    if rc == _native.FDF_ERR_CAPACITY:
+        out = np.empty((n.value, 2), dtype=np.uint32)
+        scores = np.empty(n.value, dtype=np.uint16)
+        rc = lib.fdf_detect_batch_scored(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg),
+                                         out.ctypes.data, scores.ctypes.data, out.shape[0],
+                                         offsets.ctypes.data, ctypes.byref(n))
+    check(rc, "fdf_detect_batch_scored")
+    return out[: n.value], scores[: n.value], offsets
+
+
+def score_device(frames, config, points, offsets, scores, stream=None, device=None):
+    """Scores of detect_device's output, on the device: ``points`` (cap, 2) and ``offsets``
+    as detect_device filled them, ``scores`` a (cap,) int16/uint16 CUDA tensor.
+    Asynchronous on ``stream`` (default: torch's current stream)."""
+    import torch
+
+    if frames.dim() != 3 or frames.dtype != torch.uint8 or not frames.is_contiguous():
+        raise ValueError("frames must be a contiguous (F, H, W) uint8 tensor")
+    if not (frames.is_cuda and points.is_cuda and offsets.is_cuda and scores.is_cuda):
+        raise ValueError("score_device needs CUDA (HIP) tensors")
+    if scores.element_size() != 2 or not scores.is_contiguous() or \
+            scores.numel() < points.shape[0]:
+        raise ValueError("scores must be a contiguous 16-bit tensor with cap entries")
+    if offsets.dtype != torch.int64 or offsets.numel() < frames.shape[0] + 1:
+        raise ValueError("offsets must be int64 with F+1 entries")
+    dev = frames.device.index if device is None else device
+    cfg = _to_c_config(config)
+    ctx = context(dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(frames.device)
+    f, h, w = frames.shape
+    rc = _native.load().fdf_score_device(
+        ctx.handle, frames.data_ptr(), f, w, h, h * w, ctypes.byref(cfg), points.data_ptr(),
+        points.shape[0], offsets.data_ptr(), scores.data_ptr(),
+        ctypes.c_void_p(stream.cuda_stream))
+    check(rc, "fdf_score_device")
+
+
 __all__ = ["NORTH", "EAST", "SOUTH", "WEST", "circle", "calculate_offsets", "context",
            "detect_array", "detector", "detector_batch", "detect_device", "keypoint_scores",
+           "detect_scored_array", "detector_scored", "detector_batch_scored", "score_device",
+           "detect_rgb_array", "detector_rgb", "rgb_to_luma",
            "NonMaximalSuppression"]

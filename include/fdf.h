@@ -42,7 +42,9 @@ enum fdf_status {
     FDF_ERR_NMS = 4,       /* non_maximal_supression value not 0, 1 or 2 */
     FDF_ERR_DEVICE = 5,    /* HIP runtime failure (no device, launch or copy error) */
     FDF_ERR_ARG = 6,       /* NULL pointer, stride < width, or a size that overflows */
-    FDF_ERR_ALLOC = 7      /* device or pinned host allocation failed */
+    FDF_ERR_ALLOC = 7,     /* device or pinned host allocation failed */
+    FDF_ERR_BUSY = 8,      /* pipeline: the ticket's slot still holds uncollected results */
+    FDF_ERR_DROPPED = 9    /* pipeline: a batch found more keypoints than its device capacity */
 };
 
 /* src/lib.rs:26-36 NonMaximalSuppression {Off, MaxThreshold, SumAbsolute}. */
@@ -159,6 +161,75 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
 int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
                      size_t stride_bytes, const fdf_config* cfg, const fdf_point* points,
                      size_t n_points, uint16_t* out_scores);
+
+/*
+ * Detection with scores: (x, y, score) per keypoint.  As fdf_detect / fdf_detect_batch,
+ * and out_scores[k] (`cap` entries) is point k's u16 score -- the one cfg->nms suppresses
+ * with (MaxThreshold: src/fast_simd.rs:623-718; SumAbsolute: :722-749), or the
+ * max-threshold score when NMS is off.  Scores are computed on the device from the frame
+ * already resident there; capacity semantics as fdf_detect.
+ */
+int fdf_detect_scored(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
+                      size_t stride_bytes, const fdf_config* cfg, fdf_point* out,
+                      uint16_t* out_scores, size_t cap, size_t* n_out);
+int fdf_detect_batch_scored(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames,
+                            uint32_t width, uint32_t height, size_t frame_stride_bytes,
+                            const fdf_config* cfg, fdf_point* out, uint16_t* out_scores,
+                            size_t cap, uint64_t* frame_offsets, size_t* n_out);
+
+/*
+ * Device-resident scoring of fdf_detect_device's output: d_points / d_frame_offsets as that
+ * call filled them (same frames, shape, config and `cap`), d_scores with `cap` entries.
+ * Asynchronous on `stream`; points with index >= cap are skipped.  n_frames <= 65535.
+ */
+int fdf_score_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
+                     uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
+                     const fdf_config* cfg, const fdf_point* d_points, uint64_t cap,
+                     const uint64_t* d_frame_offsets, uint16_t* d_scores, void* stream);
+
+/*
+ * Streaming host pipeline (extension; the reference's callers detect on one
+ * host image at a time, src/lib.rs:62-64, src/main.rs:58-64).  Host frames in, host
+ * keypoints out, with the host->device copy of one batch, the detection of another and the
+ * device->host copy of a third in flight together.  `depth` (1..16) batch slots, each with
+ * pinned host staging for `max_frames` frames of width x height pixels (3 bytes per pixel
+ * with FDF_PIPE_RGB, converted on the device as fdf_detect_rgb does), its own device
+ * buffers, context and HIP stream.  Device output per slot holds max_points_per_frame points
+ * per frame (0 = (width-6) * (height-6), the most a frame can have).
+ *
+ * Tickets are issued in order; ticket k uses slot k % depth, which must have been
+ * collected: fdf_pipeline_acquire returns FDF_ERR_BUSY otherwise.  A pipeline is not
+ * thread-safe beyond one producer and one consumer calling under the pipeline's own lock
+ * (every call takes it; fdf_pipeline_collect releases it while waiting on the device).
+ */
+typedef struct fdf_pipeline fdf_pipeline;
+enum fdf_pipe_flags {
+    FDF_PIPE_RGB = 1,     /* frames are RGB8 (rows of 3 * width bytes) */
+    FDF_PIPE_SCORES = 2   /* also compute each keypoint's score (as fdf_detect_scored) */
+};
+int fdf_pipeline_create(int device, uint32_t width, uint32_t height, uint32_t max_frames,
+                        uint32_t depth, uint64_t max_points_per_frame, uint32_t flags,
+                        const fdf_config* cfg, fdf_pipeline** out);
+void fdf_pipeline_destroy(fdf_pipeline* p);
+/* The pinned staging buffer of the next ticket: frame f at *frames + f * frame bytes. */
+int fdf_pipeline_acquire(fdf_pipeline* p, uint8_t** frames, uint64_t* ticket);
+/* Enqueue an acquired ticket's first n_frames (1..max_frames) frames; returns at once. */
+int fdf_pipeline_submit(fdf_pipeline* p, uint64_t ticket, uint32_t n_frames);
+/* acquire + copy n_frames frames (frame f at frames + f * frame_stride_bytes, rows packed)
+ * into the staging buffer + submit. */
+int fdf_pipeline_push(fdf_pipeline* p, const uint8_t* frames, uint32_t n_frames,
+                      size_t frame_stride_bytes, uint64_t* ticket);
+/*
+ * Wait for a submitted ticket and copy out its keypoints (frames concatenated in order, each
+ * in raster order), scores (FDF_PIPE_SCORES; `out_scores` may be NULL) and frame_offsets
+ * (n_frames + 1 entries; may be NULL).  FDF_ERR_CAPACITY: `cap` is below *n_out; nothing
+ * is released, call again with a larger buffer.  FDF_OK releases the slot.  FDF_ERR_DROPPED:
+ * the batch had *n_out points but the slot held only the first max_points_per_frame *
+ * n_frames of them (those are copied, frame_offsets are exact); the slot is released.
+ */
+int fdf_pipeline_collect(fdf_pipeline* p, uint64_t ticket, fdf_point* out,
+                         uint16_t* out_scores, size_t cap, uint64_t* frame_offsets,
+                         size_t* n_out);
 
 #ifdef __cplusplus
 }
