@@ -29,6 +29,7 @@ struct fdf_ctx {
     uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
+    uint8_t* d_map = nullptr;           size_t map_bytes = 0;      // NMS score map
     unsigned long long* d_state = nullptr; size_t state_n = 0;     // compaction look-back
     uint32_t* d_ticket = nullptr;
     uint32_t epoch = 0;
@@ -93,10 +94,9 @@ struct Geometry {
 };
 
 
-Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score_bytes) {
+Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) {
     Geometry g;
-    const uint32_t lc = (uint32_t)fdfk::lane_cols_for(score_bytes ? 1u : 0u);
-    const uint32_t sc = (uint32_t)fdfk::strip_cols((int)lc);
+    const uint32_t sc = (uint32_t)fdfk::strip_cols(fdfk::kLaneCols);
     g.nstrips = (w - 3 + sc - 1) / sc;
     // >= 4 units per band (one per wave), handed out dynamically; taller units (fewer halo
     // rows) measured faster than more, shorter units for balance
@@ -104,9 +104,10 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score
     if (const char* e = std::getenv("FDF_NSUB")) g.nsub = (uint32_t)std::strtoul(e, nullptr, 0);
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
-    // LDS per workgroup sets the workgroups per CU: 4 without NMS and for max-threshold,
-    // 3 for SAD's 16-bit score ring (tools/ablate.py sweeps).
-    uint32_t budget = score_bytes == 2 ? 53000 : 40000;
+    // extra rows a unit tests: NMS bands test one row above and below (first / last unit)
+    const uint32_t halo = fdfk::band_halo(nms) * (g.nsub == 1 ? 2u : 1u);
+    // LDS per workgroup sets the workgroups per CU: <= 40 KB keeps 4
+    uint32_t budget = 40000;
     if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the
@@ -114,17 +115,17 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t score
     double best = -1.0;
     g.R = 0;
     for (uint32_t R = g.nsub; R <= 256 && R < centre_rows + g.nsub; R += g.nsub) {
-        if (fdfk::make_sweep_layout(R, nw, score_bytes, lc).total > budget) break;
+        if (fdfk::make_sweep_layout(R, nw, nms).total > budget) break;
         const uint64_t tasks = (uint64_t)n_frames * ((centre_rows + R - 1) / R);
         if (tasks < 1024) break;
-        const uint32_t steps = fdfk::sweep_steps(R / g.nsub, score_bytes);
+        const uint32_t steps = fdfk::sweep_steps(R / g.nsub, halo);
         const double eff = (double)R / (double)(steps * g.nsub);
         if (eff > best + 1e-9) { best = eff; g.R = R; }
     }
     if (g.R == 0) {
-        const uint32_t unit = 8 - 3 - (score_bytes ? 2 : 0);
+        const uint32_t unit = 8 - 3 - halo;
         g.R = g.nsub * unit;
-        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, score_bytes, lc).total > budget)
+        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, nms).total > budget)
             g.R -= g.nsub;
     }
     return g;
@@ -135,10 +136,10 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream) {
     const uint32_t sb = fdfk::score_bytes_for(cfg->nms);
-    const Geometry geo = pick_geometry(n_frames, w, h, sb);
+    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
-    if (fdfk::make_sweep_layout(R, nw, sb, fdfk::lane_cols_for(cfg->nms)).total > fdfk::kSweepMaxLds)
+    if (fdfk::make_sweep_layout(R, nw, cfg->nms).total > fdfk::kSweepMaxLds)
         return FDF_ERR_SIZE;
     const uint32_t bands = (h - 6 + R - 1) / R;
     const uint64_t ntasks = (uint64_t)bands * n_frames;
@@ -149,6 +150,10 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     int rc;
     if ((rc = ensure(&ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), false, stream))) return rc;
     if ((rc = ensure(&ctx->d_counts, &ctx->counts_n, (size_t)ntasks, false, stream))) return rc;
+    // NMS score map: written at keypoints only and read only where the keypoint bitmap
+    // marks one, so it is never cleared
+    if (sb && (rc = ensure(&ctx->d_map, &ctx->map_bytes, (size_t)n_frames * w * h * sb, false, stream)))
+        return rc;
     if ((rc = ensure(&ctx->d_state, &ctx->state_n, (size_t)ngroups, true, stream))) return rc;
     if (!ctx->d_ticket) {
         if (hipMalloc(reinterpret_cast<void**>(&ctx->d_ticket), sizeof(uint32_t)) != hipSuccess)
@@ -179,6 +184,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.flags = dbg ? (uint32_t)std::strtoul(dbg, nullptr, 0) : 0u;
     p.nstrips = geo.nstrips;
     p.nsub = geo.nsub;
+    p.scores = ctx->d_map;
     fdfk::CompactParams c;
     c.width = w;
     c.height = h;
@@ -373,6 +379,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_scores);
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
+        (void)hipFree(ctx->d_map);
         (void)hipFree(ctx->d_state);
         (void)hipFree(ctx->d_ticket);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);

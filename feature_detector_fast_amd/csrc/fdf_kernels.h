@@ -21,63 +21,59 @@ constexpr uint32_t kFlagNoFullTest = 1;   // candidates are never tested (no key
 constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (counts only)
 constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compaction only)
 constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
+constexpr uint32_t kFlagNoNms = 16;       // NMS modes: every keypoint is kept (no band NMS pass)
 
-// Column-sweep kernel (fdf_sweep.hip): per-wave LDS region + the band bitmap.
-// Columns per lane (16; FDF_LC_NMS = 8 halves the NMS score ring for A/B runs).  A strip is
+// Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).
-#ifndef FDF_LC_NMS
-#define FDF_LC_NMS 16
-#endif
-__host__ __device__ constexpr int lane_cols_for(uint32_t nms) { return nms == 0 ? 16 : FDF_LC_NMS; }
+constexpr int kLaneCols = 16;
 __host__ __device__ constexpr int strip_cols(int lc) { return 62 * lc; }
 constexpr int kSweepPixelQ = 256;             // candidate pixel FIFO per wave (power of two)
-// NMS score ring rows per wave (power of two): deep enough that testing can lag the sweep
-// while a 64-pixel batch fills; SAD's 16-bit scores make its ring twice as big per row.
-// (4 rows of 16-column lanes measured fastest: 8 or 16 rows, or 8-column lanes, cost a
-// workgroup per CU; batches are issued partially full once their oldest pixel would
-// outrun the ring.  tools/build_variant.sh rebuilds with other values for A/B runs.)
-#ifndef FDF_RING_MAXT
-#define FDF_RING_MAXT 4
-#endif
-#ifndef FDF_RING_SAD
-#define FDF_RING_SAD 4
-#endif
-__host__ __device__ constexpr int sweep_ring_rows(uint32_t nms) {
-    return nms == 0 ? 0 : (nms == 1 ? FDF_RING_MAXT : FDF_RING_SAD);
-}
-constexpr int kSweepKpCap = 256;              // unfinalized NMS keypoints per wave
 constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per workgroup)
 
-// A full-test batch is issued every kSweepIssue(nms) rows once 64 candidates are queued and
-// is evaluated the same number of rows later.
-#ifndef FDF_ISSUE_NMS
-#define FDF_ISSUE_NMS 4
+// A full-test batch is issued every kSweepIssue rows once 64 candidates are queued and is
+// evaluated the same number of rows later.
+#ifndef FDF_ISSUE
+#define FDF_ISSUE 2
 #endif
-__host__ __device__ constexpr int sweep_issue_every(uint32_t nms) { return nms == 0 ? 2 : FDF_ISSUE_NMS; }
+constexpr int kSweepIssue = FDF_ISSUE;
 
+// Rows of keypoint bitmap above and below a band: NMS compares a band's edge rows with the
+// neighbouring bands' rows, so the band also tests one row each side (scores only).
+__host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 0u; }
+
+// LDS of one workgroup: 4 candidate FIFOs and the keypoint bitmap of the band's R rows plus
+// the NMS halo rows (NMS then clears the suppressed keypoints in place).  NMS also keeps the
+// band's keypoint scores: a list of kScoreListCap (position, score) entries, the scores
+// scattered into raster rank order, and per-row / per-8-word-block keypoint counts that
+// turn a bitmap position into its rank.
+constexpr uint32_t kScoreListCap = 2048;
 struct SweepLayout {
-    uint32_t pq, ring, kp, wave_bytes, bitmap, total;
+    uint32_t pq, wave_bytes, bitmap, slist, sranked, bprefix, rprefix, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t v);
 
-__host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw,
-                                                         uint32_t score_bytes, uint32_t lc) {
+__host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw, uint32_t nms) {
     SweepLayout L;
-    uint32_t o = 0;
-    L.pq = o;       o += kSweepPixelQ * 4;
-    L.ring = o;     o += sweep_ring_rows(score_bytes) * 64 * lc * score_bytes;
-    L.kp = o;       o += score_bytes ? kSweepKpCap * 4 : 0;
-    L.wave_bytes = align16(o);
+    const uint32_t rows = R + 2 * band_halo(nms);
+    const uint32_t nb = (nw + 7) / 8;
+    L.pq = 0;
+    L.wave_bytes = kSweepPixelQ * 4;
     L.bitmap = 4 * L.wave_bytes;
-    L.total = L.bitmap + align16(R * nw * 4) + 64;
+    L.slist = L.bitmap + align16(rows * nw * 4);
+    const uint32_t cap = nms ? kScoreListCap : 0u;
+    L.sranked = L.slist + cap * 4;
+    L.bprefix = L.sranked + cap * 2;
+    L.rprefix = L.bprefix + (nms ? align16(rows * nb * 2) : 0u);
+    L.misc = L.rprefix + (nms ? align16(rows * 4) : 0u);
+    L.total = L.misc + 64;
     return L;
 }
 
-// Sweep steps a unit of `rows` owned rows takes: the pre-filtered rows (owned rows plus, with
-// NMS, one score row each side) and 3 rows of vertical look-ahead, in whole 8-step blocks.
-__host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t score_bytes) {
-    return (rows + 3 + (score_bytes ? 2 : 0) + 7) & ~7u;
+// Sweep steps of a unit of `rows` owned rows plus `halo` extra tested rows: 3 rows of
+// vertical look-ahead, in whole 8-step blocks.
+__host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t halo) {
+    return (rows + halo + 3 + 7) & ~7u;
 }
 
 __host__ __device__ inline uint32_t align16(uint32_t v) { return (v + 15u) & ~15u; }
@@ -106,6 +102,8 @@ struct BandParams {
     uint32_t* counts;            // ntasks keypoint counts (band order = raster order)
     uint32_t flags;              // kFlag* ablation switches, 0 in production
     uint32_t nstrips, nsub;      // sweep kernel: column strips x sub-bands per band
+    uint8_t* scores;             // NMS: score map, u8 (max-t) / u16 (SAD) per pixel, frame f at
+                                 // scores + f * width * height * score bytes (written at keypoints only)
 };
 
 // Bands per compaction workgroup: enough groups (~1024) to spread the copy over the chip.

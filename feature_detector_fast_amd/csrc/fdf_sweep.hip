@@ -6,9 +6,8 @@
 // One workgroup (4 waves) owns a band of R full-width centre rows of one frame.  The band is
 // cut into units = (column strip) x (sub-band of rows); waves take units from an LDS counter
 // and sweep them top to bottom:
-//   * lane l owns LC columns (one LC-byte buffer load per row; LC = 16 without NMS, 8 with
-//     NMS, whose score ring would otherwise cut the waves per CU); lanes 0 and 63 are halo
-//     lanes that only feed their neighbours, so a strip covers 62 x LC centres;
+//   * lane l owns 16 columns (one 16-byte buffer load per row); lanes 0 and 63 are halo
+//     lanes that only feed their neighbours, so a strip covers 62 x 16 centres;
 //   * pixel rows stream through an 8-slot register ring: loads run 4 rows ahead, are never
 //     guarded by a branch and are never copied, so the compiler's vmcnt bookkeeping keeps
 //     them in flight;
@@ -23,13 +22,13 @@
 //     7x7 neighbourhood with 7 row-window loads straight from the frame (the rows were just
 //     streamed, so these hit L2).  The batch is evaluated kSweepIssue rows later -- by then
 //     the row loads issued before it are due anyway, so waiting for it never drains the row
-//     prefetch -- with the per-lane VALU segment test (fdf_common.h);
-//   * NMS: scores go to a 16-row LDS score ring per wave, keypoints of owned pixels to a
-//     list; whenever testing has caught up with more rows, the keypoints of the rows whose
-//     neighbours are all scored pass the 3x3 strict-max test (:589-616) into the workgroup's
-//     band bitmap.
-// The band's keep-bits are then written to its output slot (its points in raster order, or
-// the bitmap if they do not fit) and compact_kernel orders all slots.
+//     prefetch -- with the per-lane VALU segment test (fdf_common.h).  Keypoints set their
+//     bit in the band's LDS bitmap; with NMS their score goes to the frame's score map.
+// NMS (src/fast_simd.rs:589-616) runs once the whole band is tested: the band also tests one
+// row above and below it, so every neighbour of its keypoints is in the bitmap, and each
+// keypoint is compared with the scores of the neighbours the bitmap marks.  The band's
+// keep-bits are then written to its output slot (its points in raster order, or the bitmap
+// if they do not fit) and compact_kernel orders all slots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -100,29 +99,23 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
 
 struct SweepShared {
     uint32_t* pq;          // kSweepPixelQ FIFO of (row << 11) | (lane << 5) | flag bit
-    void* ring;            // sweep_ring_rows x 64*LC scores (NMS), row y in slot y % rows
-    uint32_t* kp;          // kSweepKpCap: (row << 10) | strip column
-    uint32_t* bitmap;      // band keep-bits, R x words_per_row
+    uint32_t* bitmap;      // band keypoints: bitmap row i = image row yb + i, words_per_row each
+    uint32_t* slist;       // NMS: the band's keypoints as (bitmap row * W + x) << 12 | score
+    uint32_t* slist_n;     // entries appended (past slist_cap: the rest went to the map)
+    uint32_t slist_cap;    // kScoreListCap, or 0 when a position does not fit 20 bits
 };
 
 struct UnitCtx {
     RowSource src;
     uint32_t t, nw;
     int S;                 // first owned centre column of the strip
-    int r0, r1;            // owned centre rows of the unit
-    int y0;                // first centre row of the band
+    int p0, p1;            // tested centre rows of the unit (owned rows plus NMS halo rows)
+    int yb;                // image row of bitmap row 0 (band start minus the NMS halo)
     uint32_t lane;
-    bool dense;            // NMS keypoint list overflowed: finalize densely
     uint32_t head, tail;   // candidate FIFO: entries [head, tail) at pq[i % kSweepPixelQ]
-    uint32_t kpn;
     uint32_t flags;        // BandParams::flags (ablation runs only)
+    uint8_t* smap;         // NMS: this frame's score map
 };
-
-template <int LC, typename ScoreT>
-__device__ __forceinline__ ScoreT* ring_at(const SweepShared& sh, int y, int cl) {
-    constexpr int kRing = sweep_ring_rows(sizeof(ScoreT));   // score bytes 1 / 2 = nms 1 / 2
-    return reinterpret_cast<ScoreT*>(sh.ring) + (y & (kRing - 1)) * (64 * LC) + cl;
-}
 
 // ---------------------------------------------------------------------------------------
 // Full test of a batch of up to 64 queued pixels, one per lane, in two halves: issue pops
@@ -184,7 +177,7 @@ __device__ __forceinline__ void pack_ring(const Batch& b, uint32_t (&w)[4], uint
     c = b.a3.x >> 24;
 }
 
-template <int NMS, int N, int LC, typename ScoreT>
+template <int NMS, int N, int LC>
 __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
                                                const LerpConsts& lk, const Batch& b) {
     const int y = (int)(b.code >> 10), cl = (int)(b.code & 1023u);
@@ -193,84 +186,33 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
     pack_ring(b, w, c);
     bool kb, kd;
     lane_segment_test_packed<N>(c, w, lk, kb, kd);
+    // every queued pixel is a centre of the unit's strip and tested rows (vmask, p0 .. p1)
     const bool is_kp = b.act && (kb || kd);
-    const bool owned = cl >= LC && cl < LC + strip_cols(LC) && y >= u.r0 && y < u.r1;
-    if constexpr (NMS == kNmsOff) {
-        if (is_kp && owned)
-            atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
-    } else {
-        if (is_kp) {
-            uint32_t p[16];
+    if (is_kp) atomicOr(&sh.bitmap[(y - u.yb) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
+    if constexpr (NMS != kNmsOff) {
+        // scores go to the band's LDS list; once it is full, to the frame's score map
+        const uint64_t bal = wave_ballot(is_kp);
+        if (bal) {
+            uint32_t base = 0;
+            if (u.lane == 0) base = atomicAdd(sh.slist_n, (uint32_t)__popcll(bal));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (is_kp) {
+                uint32_t p[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
-            const uint32_t score = NMS == kNmsMaxThreshold ? score_max_threshold<N>(c, p, kd)
-                                                           : score_sum_abs(c, p, u.t);
-            *ring_at<LC, ScoreT>(sh, y, cl) = (ScoreT)score;
-        }
-        const bool add = is_kp && owned;
-        const uint64_t bal = wave_ballot(add);
-        if (add) {
-            const uint32_t k = u.kpn + lanes_below(bal);
-            if (k < kSweepKpCap) sh.kp[k] = b.code;
-        }
-        u.kpn += (uint32_t)__popcll(bal);
-    }
-}
-
-// 3x3 strict maximum (src/fast_simd.rs:596-615).  All nine reads are issued before any
-// compare (no short-circuit), so they cost one LDS round trip, not nine.
-template <int LC, typename ScoreT>
-__device__ __forceinline__ bool nms_keep_ring(const SweepShared& sh, int y, int cl) {
-    const ScoreT* a = ring_at<LC, ScoreT>(sh, y - 1, cl);
-    const ScoreT* m = ring_at<LC, ScoreT>(sh, y, cl);
-    const ScoreT* b = ring_at<LC, ScoreT>(sh, y + 1, cl);
-    const uint32_t v = m[0];
-    const uint32_t n0 = a[-1], n1 = a[0], n2 = a[1], n3 = m[-1], n4 = m[1], n5 = b[-1],
-                   n6 = b[0], n7 = b[1];
-    const uint32_t mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
-    return v > mx;
-}
-
-// NMS: keep-bits for the unit's keypoints in rows first .. ylim (all neighbours scored).
-template <int LC, typename ScoreT>
-__device__ __forceinline__ void sweep_finalize(const SweepShared& sh, UnitCtx& u, int first,
-                                               int ylim) {
-    const int H = (int)u.src.H;
-    if (u.kpn > kSweepKpCap) u.dense = true;
-    if (u.dense) {
-        // rare: the list overflowed -- scan the owned columns of the rows densely
-        const int lo = first > u.r0 ? first : u.r0;
-        for (int y = lo; y <= ylim && y < u.r1; ++y) {
-            if (y == 3 || y == H - 4) continue;
-            if (u.lane < 1 || u.lane > 62) continue;
-            for (int j = 0; j < LC; ++j) {
-                const int cl = (int)u.lane * LC + j;
-                const int x = u.S - LC + cl;
-                if (x < 3 || x >= (int)u.src.W - 3) continue;
-                if (*ring_at<LC, ScoreT>(sh, y, cl) != 0 && nms_keep_ring<LC, ScoreT>(sh, y, cl))
-                    atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
+                for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+                const uint32_t score = NMS == kNmsMaxThreshold ? score_max_threshold<N>(c, p, kd)
+                                                               : score_sum_abs(c, p, u.t);
+                const uint32_t idx = base + lanes_below(bal);
+                if (idx < sh.slist_cap) {
+                    sh.slist[idx] = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
+                } else {
+                    const uint32_t o = (uint32_t)y * u.src.W + (uint32_t)x;
+                    if constexpr (NMS == kNmsMaxThreshold) u.smap[o] = (uint8_t)score;
+                    else reinterpret_cast<uint16_t*>(u.smap)[o] = (uint16_t)score;
+                }
             }
         }
-        u.kpn = 0;
-        return;
     }
-    uint32_t kept = 0;
-    for (uint32_t b0 = 0; b0 < u.kpn; b0 += 64) {
-        const uint32_t i = b0 + u.lane;
-        const bool act = i < u.kpn;
-        const uint32_t e = act ? sh.kp[i] : 0u;
-        const int y = (int)(e >> 10), cl = (int)(e & 1023u);
-        const bool fin = act && y <= ylim;
-        const bool carry = act && !fin;
-        const uint64_t bal = wave_ballot(carry);
-        if (carry) sh.kp[kept + lanes_below(bal)] = e;   // kept + idx <= i: read before write
-        kept += (uint32_t)__popcll(bal);
-        if (fin && y != 3 && y != H - 4 && nms_keep_ring<LC, ScoreT>(sh, y, cl)) {
-            const int x = u.S - LC + cl;
-            atomicOr(&sh.bitmap[(y - u.y0) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
-        }
-    }
-    u.kpn = kept;
 }
 
 // Horizontal/vertical comparison flags of one lane row (bit 7 of each byte, LC pixels).
@@ -292,13 +234,13 @@ __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>:
     return f;
 }
 
-// Test everything queued, now (FIFO overflow, a score-ring wrap, the end of a unit).
-template <int NMS, int N, int LC, typename ScoreT>
+// Test everything queued, now (FIFO overflow, the end of a unit).
+template <int NMS, int N, int LC>
 __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
                                             const LerpConsts& lk, bool& inflight,
                                             const Batch& batch) {
     if (inflight) {
-        evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, batch);
+        evaluate_batch<NMS, N, LC>(sh, u, lk, batch);
         inflight = false;
     }
     while (u.tail != u.head) {
@@ -307,37 +249,20 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
             break;
         }
         const Batch b = issue_batch<LC>(sh, u, min(u.tail - u.head, 64u));
-        evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, b);
-    }
-}
-
-// NMS: finalize the rows first_unfinal .. ylim (when there are any).
-template <int LC, typename ScoreT>
-__device__ __forceinline__ void finalize_upto(const SweepShared& sh, UnitCtx& u,
-                                              int& first_unfinal, int ylim) {
-    if (ylim >= first_unfinal) {
-        sweep_finalize<LC, ScoreT>(sh, u, first_unfinal, ylim);
-        first_unfinal = ylim + 1;
+        evaluate_batch<NMS, N, LC>(sh, u, lk, b);
     }
 }
 
 template <int NMS, int N, bool EXACT>
 __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
-    using ScoreT = typename std::conditional<NMS == kNmsSumAbsolute, uint16_t, uint8_t>::type;
-    constexpr int LC = lane_cols_for(NMS);
+    constexpr int LC = kLaneCols;
     constexpr int M = LC / 4;
-    constexpr int kIssue = sweep_issue_every(NMS);
-    // the oldest queued row may lag the sweep by this much before a partial batch is issued
-    // (the ring keeps rows >= (oldest untested) - 2 up to the current row)
-    constexpr int kLagLimit = NMS == kNmsOff ? 1 << 30
-                                             : (sweep_ring_rows(NMS) - kIssue - 3 > 1
-                                                    ? sweep_ring_rows(NMS) - kIssue - 3 : 1);
+    constexpr int kIssue = kSweepIssue;
     using RowV = typename LaneRow<LC>::type;
     const uint32_t lane = u.lane;
-    const int H = (int)u.src.H, W = (int)u.src.W;
+    const int W = (int)u.src.W;
     const int xb = u.S - LC + LC * (int)lane;
-    // candidate columns of this lane: owned centres, plus for NMS the two border columns the
-    // strip's edge keypoints compare against (scores only)
+    // candidate columns of this lane: the strip's centres (halo lanes 0 and 63 own none)
     // (bit 8j + m = lane column 4m + j, the order the candidate mask is built in)
     uint32_t vmask = 0;
 #pragma unroll
@@ -345,21 +270,14 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int x = xb + 4 * m + j;
-            bool ok = x >= 3 && x < W - 3;
-            if (lane == 0) ok = ok && NMS != kNmsOff && x == u.S - 1;
-            if (lane == 63) ok = ok && NMS != kNmsOff && x == u.S + strip_cols(LC);
-            if (ok) vmask |= 1u << (8 * j + m);
+            if (x >= 3 && x < W - 3 && lane >= 1 && lane <= 62) vmask |= 1u << (8 * j + m);
         }
     }
-    const int ringr = NMS == kNmsOff ? 0 : 1;
-    const int p0 = u.r0 - ringr, p1 = u.r1 + ringr;   // rows run through the pre-filter
+    const int p0 = u.p0, p1 = u.p1;                    // rows run through the pre-filter
     const int ys = p0 - 3;                             // first row of vertical comparisons
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
     u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
     u.head = u.tail = 0;
-    u.kpn = 0;
-    u.dense = false;
-    int first_unfinal = u.r0;                          // NMS: rows before it are finalized
     bool inflight = false;
     Batch batch;
 
@@ -383,7 +301,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
         const bool live = yv >= p0 && yv < p1;                                               \
-        if (live && yv >= 3 && yv < H - 3 && !(u.flags & kFlagNoLoad)) {                     \
+        if (live && !(u.flags & kFlagNoLoad)) {                                              \
             RowV e;                                                                          \
             _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
             e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
@@ -407,18 +325,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 cand[m] = br | ~nd;                                                          \
             }                                                                                \
         }                                                                                    \
-        if constexpr (NMS != kNmsOff) {                                                      \
-            if (live) {                                                                      \
-                /* the ring slot of row yv still holds row yv - 16: if that row is still */  \
-                /* needed as an NMS neighbour, catch testing and NMS up first */             \
-                if (yv - sweep_ring_rows(NMS) >= first_unfinal - 1) {                        \
-                    flush_tests<NMS, N, LC, ScoreT>(sh, u, lk, inflight, batch);             \
-                    finalize_upto<LC, ScoreT>(sh, u, first_unfinal, yv - 2);                 \
-                }                                                                            \
-                RowV* rp = reinterpret_cast<RowV*>(ring_at<LC, ScoreT>(sh, yv, LC * (int)lane)); \
-                _Pragma("unroll") for (int q = 0; q < (int)sizeof(ScoreT); ++q) rp[q] = (RowV)(0u); \
-            }                                                                                \
-        }                                                                                    \
         /* candidate pixels into the FIFO, one per lane per round: column 4m + j of the */   \
         /* lane is bit 8j + m of cm; the entry keeps the bit, issue_batch decodes it */      \
         const uint32_t code_base = ((uint32_t)yv << 11) | (lane << 5);                       \
@@ -438,33 +344,21 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             if (u.tail - u.head > kSweepPixelQ - 64) {                                       \
                 /* dense image: test the oldest batch now, synchronously */                  \
                 if (u.flags & kFlagNoFullTest) u.head += 64;                                 \
-                else evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, issue_batch<LC>(sh, u, 64u)); \
+                else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, 64u));     \
             }                                                                                \
         }                                                                                    \
         if (((J) % kIssue) == kIssue - 1) {                                                  \
             /* the batch issued kIssue rows ago is due; issue the next full one */           \
             if (inflight) {                                                                  \
-                evaluate_batch<NMS, N, LC, ScoreT>(sh, u, lk, batch);                        \
+                evaluate_batch<NMS, N, LC>(sh, u, lk, batch);                                \
                 inflight = false;                                                            \
             }                                                                                \
             const uint32_t pend = u.tail - u.head;                                           \
-            bool go = pend >= 64;                                                            \
-            if constexpr (NMS != kNmsOff) {                                                  \
-                /* a partial batch goes too once its oldest pixel would outrun the ring */   \
-                if (!go && pend > 0)                                                         \
-                    go = yv - (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 11) >= kLagLimit;  \
-            }                                                                                \
-            if (go && (u.flags & kFlagNoFullTest)) u.head += min(pend, 64u);                 \
-            const uint32_t n = (go && !(u.flags & kFlagNoFullTest)) ? min(pend, 64u) : 0u;   \
+            const bool go = pend >= 64;                                                      \
+            if (go && (u.flags & kFlagNoFullTest)) u.head += 64u;                            \
+            const uint32_t n = (go && !(u.flags & kFlagNoFullTest)) ? 64u : 0u;              \
             batch = issue_batch<LC>(sh, u, n);                                               \
             inflight = n != 0;                                                               \
-            if constexpr (NMS != kNmsOff) {                                                  \
-                /* rows before the oldest untested candidate are fully tested */             \
-                int r = yv + 1;                                                              \
-                if (u.tail != u.head) r = (int)(sh.pq[u.head & (kSweepPixelQ - 1)] >> 11);   \
-                if (inflight) r = min(r, (int)(__builtin_amdgcn_readfirstlane(batch.code) >> 10)); \
-                finalize_upto<LC, ScoreT>(sh, u, first_unfinal, r - 2);                      \
-            }                                                                                \
         }                                                                                    \
     }
 
@@ -479,25 +373,310 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         FDF_SWEEP_STEP(7)
     }
 #undef FDF_SWEEP_STEP
-    flush_tests<NMS, N, LC, ScoreT>(sh, u, lk, inflight, batch);
-    if constexpr (NMS != kNmsOff) finalize_upto<LC, ScoreT>(sh, u, first_unfinal, p1 - 2);
+    flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
+}
+
+// Three bitmap bits of one bitmap row: columns x-1, x, x+1 (x-1 >= 2, x+1 < W - 3).
+__device__ __forceinline__ uint32_t bits3(const uint32_t* row, int x) {
+    const int xm = x - 1, wi = xm >> 5, sh = xm & 31;
+    uint32_t v = row[wi] >> sh;
+    if (sh > 29) v |= row[wi + 1] << (32 - sh);
+    return v & 7u;
+}
+
+// Strict 3x3 maximum of one keypoint (src/fast_simd.rs:596-615): keep iff its score is above
+// the score of every neighbouring keypoint (non-keypoints score 0, ties suppress both).
+// `up`, `mid`, `dn`: neighbour bits of rows y-1, y, y+1 (bit k = column x-1+k).
+template <int NMS>
+__device__ __forceinline__ bool nms_keep(const __amdgpu_buffer_rsrc_t& map, uint32_t W, int x,
+                                         int y, uint32_t up, uint32_t mid, uint32_t dn) {
+    if ((up | mid | dn) == 0) return true;
+    const uint32_t o = (uint32_t)(y - 1) * W + (uint32_t)(x - 1);   // score of (x-1, y-1)
+    uint32_t s[3][3];
+    if constexpr (NMS == kNmsMaxThreshold) {
+        const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(map, o, 0, 0);
+        const uint32_t m = __builtin_amdgcn_raw_buffer_load_b32(map, o + W, 0, 0);
+        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(map, o + 2 * W, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            s[0][k] = (a >> (8 * k)) & 0xffu;
+            s[1][k] = (m >> (8 * k)) & 0xffu;
+            s[2][k] = (d >> (8 * k)) & 0xffu;
+        }
+    } else {
+        const u32x2 a = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * o, 0, 0));
+        const u32x2 m = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * (o + W), 0, 0));
+        const u32x2 d = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * (o + 2 * W), 0, 0));
+        s[0][0] = a.x & 0xffffu; s[0][1] = a.x >> 16; s[0][2] = a.y & 0xffffu;
+        s[1][0] = m.x & 0xffffu; s[1][1] = m.x >> 16; s[1][2] = m.y & 0xffffu;
+        s[2][0] = d.x & 0xffffu; s[2][1] = d.x >> 16; s[2][2] = d.y & 0xffffu;
+    }
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        mx = max(mx, (up >> k) & 1u ? s[0][k] : 0u);
+        mx = max(mx, (mid >> k) & 1u ? s[1][k] : 0u);
+        mx = max(mx, (dn >> k) & 1u ? s[2][k] : 0u);
+    }
+    return s[1][1] > mx;
+}
+
+// Pass 1 of band_nms: the band's keypoints that have a neighbouring keypoint, as
+// r * W + x (band row r), into list[0 .. cap); returns how many there are (even past cap).
+__device__ __forceinline__ uint32_t nms_collect(const uint32_t* bitmap, uint32_t nwords,
+                                                uint32_t nw, uint32_t W, uint32_t* list,
+                                                uint32_t cap, uint32_t* list_n) {
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) *list_n = 0;
+    __syncthreads();
+    for (uint32_t w = tid; w < nwords; w += kThreads) {
+        const uint32_t r = w / nw;                       // band row; bitmap row r + 1
+        uint32_t bits = bitmap[w + nw];
+        const uint32_t* above = bitmap + r * nw;
+        while (bits) {
+            const uint32_t bit = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const int x = (int)((w - r * nw) * 32 + bit);
+            if ((bits3(above, x) | (bits3(above + nw, x) & 5u) | bits3(above + 2 * nw, x)) == 0)
+                continue;
+            const uint32_t i = atomicAdd(list_n, 1u);
+            if (i < cap) list[i] = r * W + (uint32_t)x;
+        }
+    }
+    __syncthreads();
+    return *list_n;
+}
+
+// Pass 2 + 3 of band_nms on a complete list (LDS or global): compare, then clear.
+template <int NMS>
+__device__ __forceinline__ void nms_listed(uint32_t* bitmap, uint32_t nw, uint32_t y0,
+                                           uint32_t W, const __amdgpu_buffer_rsrc_t& map,
+                                           uint32_t* list, uint32_t n_list) {
+    constexpr int kNmsUnroll = 4;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i0 = tid; i0 < n_list; i0 += kNmsUnroll * kThreads) {
+        u32x2 s[kNmsUnroll][3];     // scores of columns x-1 .. x+1, rows y-1 .. y+1
+        int xs[kNmsUnroll], rs[kNmsUnroll];
+#pragma unroll
+        for (int k = 0; k < kNmsUnroll; ++k) {
+            const uint32_t i = i0 + k * kThreads;
+            const uint32_t e = i < n_list ? list[i] : W + 3u;   // inactive: a harmless centre
+            rs[k] = (int)(e / W);
+            xs[k] = (int)(e - (uint32_t)rs[k] * W);
+            const uint32_t o = (y0 + rs[k] - 1) * W + (uint32_t)xs[k] - 1;   // (x-1, y-1)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                if constexpr (NMS == kNmsMaxThreshold)
+                    s[k][d].x = __builtin_amdgcn_raw_buffer_load_b32(map, o + d * W, 0, 0);
+                else
+                    s[k][d] = __builtin_bit_cast(
+                        u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * (o + d * W), 0, 0));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kNmsUnroll; ++k) {
+            const uint32_t i = i0 + k * kThreads;
+            if (i < n_list) {
+                const int x = xs[k];
+                const uint32_t* above = bitmap + rs[k] * nw;
+                const uint32_t nb[3] = {bits3(above, x), bits3(above + nw, x) & 5u,
+                                        bits3(above + 2 * nw, x)};
+                uint32_t mx = 0, own = 0;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        uint32_t v;
+                        if constexpr (NMS == kNmsMaxThreshold)
+                            v = (s[k][d].x >> (8 * c)) & 0xffu;
+                        else
+                            v = c == 2 ? (s[k][d].y & 0xffffu) : (s[k][d].x >> (16 * c)) & 0xffffu;
+                        if (d == 1 && c == 1) own = v;
+                        mx = max(mx, (nb[d] >> c) & 1u ? v : 0u);
+                    }
+                }
+                if (own <= mx) list[i] |= 0x80000000u;   // suppressed
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n_list; i += kThreads) {
+        const uint32_t e = list[i];
+        if (e & 0x80000000u) {
+            const uint32_t v = e & 0x7fffffffu, r = v / W, x = v - r * W;
+            atomicAnd(&bitmap[(r + 1) * nw + (x >> 5)], ~(1u << (x & 31)));
+        }
+    }
+}
+
+// Band NMS (src/fast_simd.rs:589-616) in place on the keypoint bitmap: bitmap row 0 and
+// rows + 1 are the rows just outside the band (neighbours only).  Keypoints without
+// neighbouring keypoints are kept outright.  The others are listed -- in LDS (`lds_list`,
+// the FIFO area, free now), or when that is too small in the band's output slot
+// (`scratch`) -- and compared with their neighbours' scores from the score map, kNmsUnroll
+// per thread with all their loads in flight together; the suppressed ones are cleared once
+// every comparison has read the bitmap.  A band with more such keypoints than the slot holds
+// (dense images) computes its keep-bits word by word into the slot and copies them back.
+// Rows 3 and h-4 are never output (:590-592, :342).
+template <int NMS>
+__device__ void band_nms(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                         uint32_t H, uint8_t* smap, uint32_t* lds_list, uint32_t lds_cap,
+                         uint32_t* list_n, uint32_t* scratch, uint32_t scratch_cap) {
+    constexpr uint32_t sbytes = NMS == kNmsSumAbsolute ? 2u : 1u;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nwords = rows * nw;
+    const __amdgpu_buffer_rsrc_t map =
+        __builtin_amdgcn_make_buffer_rsrc(smap, 0, (int)(W * H * sbytes), 0x00020000);
+    uint32_t n = nms_collect(bitmap, nwords, nw, W, lds_list, lds_cap, list_n);
+    if (n <= lds_cap) {
+        nms_listed<NMS>(bitmap, nw, y0, W, map, lds_list, n);
+    } else if (n <= scratch_cap) {
+        n = nms_collect(bitmap, nwords, nw, W, scratch, scratch_cap, list_n);
+        nms_listed<NMS>(bitmap, nw, y0, W, map, scratch, n);
+    } else {
+        // dense band: keep-bits word by word (serial score loads), via the slot
+        for (uint32_t w = tid; w < nwords; w += kThreads) {
+            const uint32_t r = w / nw;
+            uint32_t bits = bitmap[w + nw], kept = bits;
+            const uint32_t* above = bitmap + r * nw;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const int x = (int)((w - r * nw) * 32 + bit);
+                if (!nms_keep<NMS>(map, W, x, (int)(y0 + r), bits3(above, x),
+                                   bits3(above + nw, x) & 5u, bits3(above + 2 * nw, x)))
+                    kept &= ~(1u << bit);
+            }
+            scratch[w] = kept;
+        }
+        __syncthreads();
+        for (uint32_t w = tid; w < nwords; w += kThreads) bitmap[w + nw] = scratch[w];
+    }
+    __syncthreads();
+    // rows 3 and h - 4 keep no keypoints (they were neighbours only)
+    for (uint32_t r = 0; r < rows; ++r) {
+        const uint32_t y = y0 + r;
+        if (y != 3 && y != H - 4) continue;
+        for (uint32_t w = tid; w < nw; w += kThreads) bitmap[(r + 1) * nw + w] = 0;
+    }
+    __syncthreads();
+}
+
+// Raster rank of bitmap position (row, x): keypoints before it in the band's bitmap.
+// rprefix[row] counts the rows above, bprefix[row * nb + k] the words [0, 8k) of the row.
+__device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const uint16_t* bprefix,
+                                                const uint32_t* rprefix, uint32_t nw, uint32_t nb,
+                                                uint32_t row, uint32_t x) {
+    const uint32_t wi = x >> 5, blk = wi >> 3;
+    const uint32_t* rw = bitmap + row * nw;
+    uint32_t r = rprefix[row] + bprefix[row * nb + blk];
+    for (uint32_t j = 8 * blk; j < wi; ++j) r += __popc(rw[j]);
+    return r + __popc(rw[wi] & ((1u << (x & 31)) - 1u));
+}
+
+// Band NMS (src/fast_simd.rs:589-616) from the LDS score list, in place on the keypoint
+// bitmap (bitmap rows 0 and rows + 1 are the rows just outside the band, neighbours only).
+// The list holds every keypoint of the bitmap once; its scores are scattered into raster
+// rank order, then each keypoint of the band's own rows reads its neighbours' scores by
+// rank, and the suppressed ones are cleared once every comparison has read the bitmap.
+// Rows 3 and h-4 are never output (:590-592, :342).
+template <int NMS>
+__device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                             uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
+                             uint16_t* bprefix, uint32_t* rprefix) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t R2 = rows + 2, nb = (nw + 7) / 8;
+    for (uint32_t i = tid; i < R2 * nb; i += kThreads) {
+        const uint32_t row = i / nb, k = i - row * nb;
+        const uint32_t* rw = bitmap + row * nw;
+        uint32_t cnt = 0;
+        for (uint32_t j = 8 * k; j < min(8 * k + 8, nw); ++j) cnt += __popc(rw[j]);
+        bprefix[i] = (uint16_t)cnt;
+    }
+    __syncthreads();
+    for (uint32_t row = tid; row < R2; row += kThreads) {
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < nb; ++k) {
+            const uint32_t c = bprefix[row * nb + k];
+            bprefix[row * nb + k] = (uint16_t)acc;
+            acc += c;
+        }
+        rprefix[row] = acc;
+    }
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of the row totals
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < R2; base += 64) {
+            const uint32_t v = base + lane < R2 ? rprefix[base + lane] : 0u;
+            uint32_t incl = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(incl, d, 64);
+                if (lane >= (uint32_t)d) incl += o;
+            }
+            if (base + lane < R2) rprefix[base + lane] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) {
+        const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
+        sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb, row, x)] = (uint16_t)(e & 0xfffu);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) {
+        const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
+        if (row == 0 || row == R2 - 1) continue;          // rows outside the band
+        const uint32_t y = y0 - 1 + row;
+        const uint32_t own = e & 0xfffu;
+        uint32_t mx = 0;
+        const uint32_t mid = bits3(bitmap + row * nw, (int)x);
+        if (mid & 5u) {
+            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb, row, x);
+            if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
+            if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
+        }
+#pragma unroll
+        for (int d = -1; d <= 1; d += 2) {
+            const uint32_t nbits = bits3(bitmap + (row + d) * nw, (int)x);
+            if (nbits) {
+                uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb, row + d, x - 1);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    if ((nbits >> k) & 1u) {
+                        mx = max(mx, (uint32_t)sranked[r]);
+                        ++r;
+                    }
+                }
+            }
+        }
+        const bool suppressed = own <= mx || y == 3 || y == H - 4;
+        slist[i] = (e & ~0xfffu) | (suppressed ? 1u : 0u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) {
+        const uint32_t e = slist[i];
+        if (e & 1u) {
+            const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+            atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
+        }
+    }
+    __syncthreads();
 }
 
 // Occupancy target: 4 workgroups (16 waves) per CU, registers <= 128 VGPRs.
-template <int NMS>
-constexpr int sweep_waves_per_eu() { return 4; }
-
 template <int NMS, int N>
 __global__ __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(sweep_waves_per_eu<NMS>(), sweep_waves_per_eu<NMS>())))
+__attribute__((amdgpu_waves_per_eu(4, 4)))
 void fast_sweep_kernel(BandParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    constexpr int LC = lane_cols_for(NMS);
-    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, score_bytes_for(NMS), LC);
+    constexpr int LC = kLaneCols;
+    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, NMS);
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
     const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
+    constexpr uint32_t halo = NMS == kNmsOff ? 0u : 1u;
 
     // XCD-aware static task mapping: consecutive bands of a frame land on one XCD (its L2
     // then serves the halo rows two neighbouring bands share)
@@ -510,22 +689,26 @@ void fast_sweep_kernel(BandParams P) {
     const uint32_t rows = min(P.rows, H - 3 - y0);
 
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap);
-    uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap + align16(P.rows * nw * 4));
+    uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.misc);
     if (P.threshold >= 255) {                                        // no pixel can pass
         if (tid == 0) P.counts[task] = 0;
         return;
     }
     uint32_t* unit_ctr = wave_sum + kWaves;
-    for (uint32_t i = tid; i < rows * nw; i += kThreads) bitmap[i] = 0;
-    if (tid == 0) *unit_ctr = 0;
+    for (uint32_t i = tid; i < (rows + 2 * halo) * nw; i += kThreads) bitmap[i] = 0;
+    if (tid == 0) {
+        unit_ctr[0] = 0;
+        unit_ctr[1] = 0;
+    }
     __syncthreads();
 
-    uint8_t* wbase = smem_raw + wave * L.wave_bytes;
     SweepShared sh;
-    sh.pq = reinterpret_cast<uint32_t*>(wbase + L.pq);
-    sh.ring = wbase + L.ring;
-    sh.kp = reinterpret_cast<uint32_t*>(wbase + L.kp);
+    sh.pq = reinterpret_cast<uint32_t*>(smem_raw + L.pq + wave * L.wave_bytes);
     sh.bitmap = bitmap;
+    sh.slist = reinterpret_cast<uint32_t*>(smem_raw + L.slist);
+    sh.slist_n = unit_ctr + 1;
+    // list positions are (bitmap row * W + x) in 20 bits
+    sh.slist_cap = (uint64_t)(rows + 2 * halo) * W <= (1u << 20) ? kScoreListCap : 0u;
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
@@ -536,9 +719,11 @@ void fast_sweep_kernel(BandParams P) {
         const_cast<uint8_t*>(img), 0, (int)(W * H + 15), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_exact = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(img), 0, (int)(W * H), 0x00020000);
+    constexpr uint32_t sbytes = NMS == kNmsSumAbsolute ? 2u : 1u;
+    u.smap = P.scores + (uint64_t)frame * W * H * sbytes;
     u.t = P.threshold;
     u.nw = nw;
-    u.y0 = (int)y0;
+    u.yb = (int)(y0 - halo);
     u.lane = lane;
     u.flags = P.flags;
     const LerpConsts lk = lerp_consts(P.threshold);
@@ -560,12 +745,14 @@ void fast_sweep_kernel(BandParams P) {
                 const int num = (int)(W * H) - last_end;
                 u.src.tail_row = num < 0 ? 0 : num / (int)W + 1;
             }
-            u.r0 = (int)(y0 + sub * sub_rows);
-            u.r1 = (int)min(y0 + (sub + 1) * sub_rows, y0 + rows);
-            if (u.r0 >= u.r1) continue;
-            // rows the sweep loads: up to r1 + ringr + 2
-            const int ringr = NMS == kNmsOff ? 0 : 1;
-            if (last_frame && u.r1 + ringr + 2 >= u.src.tail_row) {
+            const int r0 = (int)(y0 + sub * sub_rows);
+            const int r1 = (int)min(y0 + (sub + 1) * sub_rows, y0 + rows);
+            if (r0 >= r1) continue;
+            // NMS: the band's first and last units also test the rows just outside the band
+            u.p0 = (halo && sub == 0 && r0 > 3) ? r0 - 1 : r0;
+            u.p1 = (halo && r1 == (int)(y0 + rows) && r1 < (int)H - 3) ? r1 + 1 : r1;
+            // rows the sweep loads: up to p1 + 2
+            if (last_frame && u.p1 + 2 >= u.src.tail_row) {
                 u.src.rs = rs_exact;
                 sweep_unit<NMS, N, true>(sh, u, lk);
             } else {
@@ -576,12 +763,38 @@ void fast_sweep_kernel(BandParams P) {
     }
     __syncthreads();
 
-    // ---- count keep-bits and write the band slot
     const uint32_t nwords = rows * nw;
+    if constexpr (NMS != kNmsOff) {
+        const uint32_t n = *sh.slist_n;
+        if (P.flags & kFlagNoNms) {
+        } else if (n <= sh.slist_cap) {
+            band_nms_lds<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, n,
+                              reinterpret_cast<uint16_t*>(smem_raw + L.sranked),
+                              reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix));
+        } else {
+            // more keypoints than the list holds: the listed scores join the score map
+            for (uint32_t i = tid; i < sh.slist_cap; i += kThreads) {
+                const uint32_t e = sh.slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
+                const uint32_t o = (y0 - 1 + row) * W + x;
+                if constexpr (NMS == kNmsMaxThreshold) u.smap[o] = (uint8_t)(e & 0xfffu);
+                else reinterpret_cast<uint16_t*>(u.smap)[o] = (uint16_t)(e & 0xfffu);
+            }
+            __syncthreads();
+            band_nms<NMS>(bitmap, rows, nw, y0, W, H, u.smap,
+                          reinterpret_cast<uint32_t*>(smem_raw + L.pq), kWaves * L.wave_bytes / 4,
+                          unit_ctr + 2, reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
+                          P.slot_bytes / 4);
+        }
+        // the band's own rows are now its keep-bits
+    }
+    const uint32_t* keep = bitmap + halo * nw;
+
+    // ---- count keep-bits and write the band slot
     const uint32_t per = (nwords + kThreads - 1) / kThreads;
     const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);
     uint32_t mine = 0;
-    for (uint32_t w = w_lo; w < w_hi; ++w) mine += __popc(bitmap[w]);
+    for (uint32_t w = w_lo; w < w_hi; ++w) mine += __popc(keep[w]);
     uint32_t incl = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -604,7 +817,7 @@ void fast_sweep_kernel(BandParams P) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
         uint32_t idx = before + incl - mine;
         for (uint32_t w = w_lo; w < w_hi; ++w) {
-            uint32_t bits = bitmap[w];
+            uint32_t bits = keep[w];
             const uint32_t r = w / nw;
             const uint32_t xb = (w - r * nw) * 32;
             while (bits) {
@@ -615,7 +828,7 @@ void fast_sweep_kernel(BandParams P) {
         }
     } else {
         uint32_t* words = reinterpret_cast<uint32_t*>(slot);
-        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = bitmap[w];
+        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
     }
 }
 
@@ -645,8 +858,7 @@ hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream
         default: break;
     }
     if (!fn) return hipErrorInvalidValue;
-    const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, score_bytes_for(nms),
-                                            lane_cols_for(nms));
+    const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, nms);
     if (L.total > kSweepMaxLds) return hipErrorInvalidValue;
     if (L.total > kMaxLds) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
