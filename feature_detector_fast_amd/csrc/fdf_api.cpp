@@ -123,7 +123,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) 
         if (eff > best + 1e-9) { best = eff; g.R = R; }
     }
     if (g.R == 0) {
-        const uint32_t unit = 8 - 3 - halo;
+        const uint32_t unit = fdfk::kSweepRing - 3 - halo;
         g.R = g.nsub * unit;
         while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, nms).total > budget)
             g.R -= g.nsub;

@@ -39,6 +39,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 // Per-launch byte constants of the lerp comparisons (threshold t < 255).
 struct LerpConsts {
     uint32_t rb, kb, rd, kd;
+    uint32_t kb0, kd0;   // pre-filter (rounding 0 for both polarities), see prefilter_compare
 };
 __device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
     LerpConsts k;
@@ -47,6 +48,12 @@ __device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
     k.kb = (128u - ((t + ob) >> 1)) * 0x01010101u;
     k.rd = od * 0x01010101u;
     k.kd = (255u - ((254u - t + od) >> 1)) * 0x01010101u;
+    // With D = x - c + 255 and v = lerp(x, ~c, 0) = D >> 1, bit 7 of lerp(v, 256 - k, 0) is
+    // D >= 2k.  Bright is D >= t + 256 and not-dark is D >= 255 - t; the threshold of the
+    // odd one is rounded so that bright flags only gain pixels and not-dark flags only lose
+    // them, i.e. the pre-filter only gains candidates: k = (t + 256) / 2, (256 - t) / 2.
+    k.kb0 = (256u - ((t + 256u) >> 1)) * 0x01010101u;
+    k.kd0 = (256u - ((256u - t) >> 1)) * 0x01010101u;
     return k;
 }
 

@@ -33,9 +33,20 @@ constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per work
 // A full-test batch is issued every kSweepIssue rows once 64 candidates are queued and is
 // evaluated the same number of rows later.
 #ifndef FDF_ISSUE
-#define FDF_ISSUE 2
+#define FDF_ISSUE 3
 #endif
 constexpr int kSweepIssue = FDF_ISSUE;
+// Pixel-row register ring of the sweep (rows in flight = kSweepRing - 4); unit sweeps are
+// whole multiples of kSweepRing steps.
+#ifndef FDF_RING
+#define FDF_RING 8
+#endif
+constexpr int kSweepRing = FDF_RING;
+// Waves per SIMD of the sweep kernel (register budget 512 / kSweepWavesPerEU VGPRs).
+#ifndef FDF_WAVES_PER_EU
+#define FDF_WAVES_PER_EU 4
+#endif
+constexpr int kSweepWavesPerEU = FDF_WAVES_PER_EU;
 
 // Rows of keypoint bitmap above and below a band: NMS compares a band's edge rows with the
 // neighbouring bands' rows, so the band also tests one row each side (scores only).
@@ -71,9 +82,9 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
 }
 
 // Sweep steps of a unit of `rows` owned rows plus `halo` extra tested rows: 3 rows of
-// vertical look-ahead, in whole 8-step blocks.
+// vertical look-ahead, in whole kSweepRing-step blocks.
 __host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t halo) {
-    return (rows + halo + 3 + 7) & ~7u;
+    return (rows + halo + 3 + kSweepRing - 1) / kSweepRing * kSweepRing;
 }
 
 __host__ __device__ inline uint32_t align16(uint32_t v) { return (v + 15u) & ~15u; }

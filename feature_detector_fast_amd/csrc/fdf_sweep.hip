@@ -8,9 +8,9 @@
 // and sweep them top to bottom:
 //   * lane l owns 16 columns (one 16-byte buffer load per row); lanes 0 and 63 are halo
 //     lanes that only feed their neighbours, so a strip covers 62 x 16 centres;
-//   * pixel rows stream through an 8-slot register ring: loads run 4 rows ahead, are never
-//     guarded by a branch and are never copied, so the compiler's vmcnt bookkeeping keeps
-//     them in flight;
+//   * pixel rows stream through a register ring of kSweepRing slots: kSweepRing - 4 row loads
+//     are in flight, none is guarded by a branch and none is copied, so the compiler's vmcnt
+//     bookkeeping keeps them in flight;
 //   * every pairwise comparison is made once and used by both of its pixels: the vertical
 //     pair (I(y), I(y+3)) gives S-flags for row y and N-flags for row y+3, the horizontal
 //     pair (I(x), I(x+3)) gives E-flags for x and W-flags for x+3 (a 3-byte shift, with the
@@ -137,17 +137,24 @@ template <int LC>
 __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, uint32_t n) {
     Batch b;
     b.act = u.lane < n;
-    // FIFO entry (row << 11) | (lane << 5) | bit, bit 8j + m = lane column 4m + j  ->
-    // the test's code (row << 10) | strip column
-    const uint32_t e = b.act ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
-    const uint32_t bit = e & 31u;
-    b.code = ((e >> 11) << 10) | (((e >> 5) & 63u) * LC + 4 * (bit & 7u) + (bit >> 3));
-    u.head += n;
     const int W = (int)u.src.W;
-    // inactive lanes read around centre (3, 3), which every tested frame has
-    const int y = b.act ? (int)(b.code >> 10) : 3;
-    const int x = b.act ? u.S - LC + (int)(b.code & 1023u) : 3;
-    const int o = (y - 3) * W + x;                              // pixel (x, y - 3)
+    // inactive lanes read around centre (3, 3), which every tested frame has; an empty batch
+    // (n = 0, wave-uniform) skips the FIFO read and the decoding
+    int o = 3 * W + 3 - 3 * W;                                  // pixel (x, y - 3) of (3, 3)
+    b.code = 0;
+    if (n != 0) {
+        // FIFO entry (row << 11) | (lane << 5) | bit, bit 8j + m = lane column 4m + j  ->
+        // the test's code (row << 10) | strip column
+        const uint32_t e = b.act ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
+        const uint32_t bit = e & 31u;
+        b.code = ((e >> 11) << 10) | (((e >> 5) & 63u) * LC + 4 * (bit & 7u) + (bit >> 3));
+        u.head += n;
+        if (b.act) {
+            const int y = (int)(b.code >> 10);
+            const int x = u.S - LC + (int)(b.code & 1023u);
+            o = (y - 3) * W + x;
+        }
+    }
     // the windows stay inside the frame: rows y-3 .. y+3 are rows, and the 1-2 bytes past
     // a row end (rows y-1 .. y+2 only) belong to the next row
     b.a0 = __builtin_amdgcn_raw_buffer_load_b32(u.src.rs, o - 1, 0, 0);
@@ -221,6 +228,11 @@ struct RowFlags {
     typename LaneRow<LC>::type b, nd;
 };
 
+// Pre-filter comparisons of one lane row (bit 7 of each byte).  FDF_SHARED_LERP: one first
+// lerp for both polarities (fdf_common.h lerp_consts kb0/kd0): `b` flags are a superset of
+// x - c > t and `nd` flags a subset of NOT(x - c < -t), so the cardinal test only gains
+// candidates -- 8 lerps a step fewer, but more candidates on images with exact-threshold
+// steps (measured slower on S1).  Default: the exact comparisons.
 template <int LC>
 __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>::type& x,
                                                      const typename LaneRow<LC>::type& nc,
@@ -228,8 +240,14 @@ __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>:
     RowFlags<LC> f;
 #pragma unroll
     for (int m = 0; m < LC / 4; ++m) {
+#ifdef FDF_SHARED_LERP
+        const uint32_t v = lerp_u8(x[m], nc[m], 0u);
+        f.b[m] = lerp_u8(v, k.kb0, 0);
+        f.nd[m] = lerp_u8(v, k.kd0, 0);
+#else
         f.b[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rb), k.kb, 0);   // x - c > t
         f.nd[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rd), k.kd, 0);  // NOT(x - c < -t)
+#endif
     }
     return f;
 }
@@ -281,13 +299,15 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     bool inflight = false;
     Batch batch;
 
-    // One 8-slot ring of pixel rows: row r in slot (r - ys) & 7.  At step J (row yv) it holds
-    // rows yv .. yv+6 with yv+4 .. yv+6 still loading, and row yv+7 is loaded into the slot
-    // of row yv-1, which is dead.  Nothing is copied, so every slot keeps its registers
-    // across loop iterations and no wait is needed for a register move.
-    RowV Rw[8];
+    // One kSweepRing-slot ring of pixel rows: row r in slot (r - ys) % kSweepRing.  At step J
+    // (row yv) it holds rows yv .. yv+K-2 (K = kSweepRing) with yv+4 .. yv+K-2 still loading,
+    // and row yv+K-1 is loaded into the slot of row yv-1, which is dead.  Nothing is copied,
+    // so every slot keeps its registers across loop iterations and no wait is needed for a
+    // register move.  The loop body is K steps, so unit sweeps are whole multiples of K.
+    constexpr int K = kSweepRing;
+    RowV Rw[K];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
+    for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
@@ -295,9 +315,9 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
         RowV cand = (RowV)(0u);                                                              \
-        Rw[((J) + 7) & 7] = load_row<LC, EXACT>(u.src, yv + 7, xb);                          \
-        const RowV s = Rw[((J) + 3) & 7];                  /* row yv + 3 */                  \
-        const RowV c = Rw[(J) & 7];                        /* row yv */                      \
+        Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);                  \
+        const RowV s = Rw[((J) + 3) % K];                  /* row yv + 3 */                  \
+        const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
         const bool live = yv >= p0 && yv < p1;                                               \
@@ -362,7 +382,8 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         }                                                                                    \
     }
 
-    for (int i0 = 0; i0 < T; i0 += 8) {
+    static_assert(K == 8 || K == 12 || K == 16, "ring of 8, 12 or 16 rows");
+    for (int i0 = 0; i0 < T; i0 += K) {
         FDF_SWEEP_STEP(0)
         FDF_SWEEP_STEP(1)
         FDF_SWEEP_STEP(2)
@@ -371,6 +392,18 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         FDF_SWEEP_STEP(5)
         FDF_SWEEP_STEP(6)
         FDF_SWEEP_STEP(7)
+        if constexpr (K >= 12) {
+            FDF_SWEEP_STEP(8)
+            FDF_SWEEP_STEP(9)
+            FDF_SWEEP_STEP(10)
+            FDF_SWEEP_STEP(11)
+        }
+        if constexpr (K >= 16) {
+            FDF_SWEEP_STEP(12)
+            FDF_SWEEP_STEP(13)
+            FDF_SWEEP_STEP(14)
+            FDF_SWEEP_STEP(15)
+        }
     }
 #undef FDF_SWEEP_STEP
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
@@ -664,10 +697,10 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
     __syncthreads();
 }
 
-// Occupancy target: 4 workgroups (16 waves) per CU, registers <= 128 VGPRs.
+// Occupancy target: kSweepWavesPerEU waves per SIMD (4: 128 VGPRs each, 2: 256).
 template <int NMS, int N>
 __global__ __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(4, 4)))
+__attribute__((amdgpu_waves_per_eu(kSweepWavesPerEU, kSweepWavesPerEU)))
 void fast_sweep_kernel(BandParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     constexpr int LC = kLaneCols;

@@ -147,6 +147,24 @@ def test_lerp_byte_comparisons_exact():
         assert np.array_equal(~not_dark, x < c - t), t
 
 
+def test_lerp_prefilter_comparisons_relaxed():
+    """The sweep's pre-filter shares one lerp between both polarities (compare_rows with
+    lerp_consts().kb0/kd0): its bright flags contain X - c > t and its dark flags contain
+    X - c < -t, widened by at most one grey level, so the cardinal test can only gain
+    candidates."""
+    c = np.arange(256)[:, None]
+    x = np.arange(256)[None, :]
+    for t in range(255):
+        kb0 = 256 - ((t + 256) >> 1)
+        kd0 = 256 - ((256 - t) >> 1)
+        v = _lerp(x, 255 - c, 0)
+        bright = _lerp(v, np.full((256, 256), kb0), 0) >= 128
+        dark = ~(_lerp(v, np.full((256, 256), kd0), 0) >= 128)
+        assert np.all(bright[x > c + t]) and np.all(dark[x < c - t]), t
+        assert np.array_equal(bright, x >= c + t + (t + 1) % 2), t
+        assert np.array_equal(dark, x <= c - t - t % 2), t
+
+
 def _prefilter(ring, c, t, n):
     card = [ring[0], ring[4], ring[8], ring[12]]
     b = [p > c + t for p in card]
