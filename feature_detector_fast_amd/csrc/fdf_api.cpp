@@ -30,9 +30,6 @@ struct fdf_ctx {
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
     uint8_t* d_map = nullptr;           size_t map_bytes = 0;      // NMS score map
-    unsigned long long* d_state = nullptr; size_t state_n = 0;     // compaction look-back
-    uint32_t* d_ticket = nullptr;
-    uint32_t epoch = 0;
     // optional per-kernel timing (fdf_ctx_set_timing): 3 events around each call's launches
     bool timing = false;
     size_t timed = 0;                     // calls recorded since timing was enabled
@@ -146,7 +143,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
     const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw);
     const uint32_t tpg = fdfk::compact_tasks_per_group((uint32_t)ntasks);
-    const uint64_t ngroups = (ntasks + tpg - 1) / tpg;
     int rc;
     if ((rc = ensure(&ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), false, stream))) return rc;
     if ((rc = ensure(&ctx->d_counts, &ctx->counts_n, (size_t)ntasks, false, stream))) return rc;
@@ -154,19 +150,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     // marks one, so it is never cleared
     if (sb && (rc = ensure(&ctx->d_map, &ctx->map_bytes, (size_t)n_frames * w * h * sb, false, stream)))
         return rc;
-    if ((rc = ensure(&ctx->d_state, &ctx->state_n, (size_t)ngroups, true, stream))) return rc;
-    if (!ctx->d_ticket) {
-        if (hipMalloc(reinterpret_cast<void**>(&ctx->d_ticket), sizeof(uint32_t)) != hipSuccess)
-            return FDF_ERR_ALLOC;
-        if (hipMemsetAsync(ctx->d_ticket, 0, sizeof(uint32_t), stream) != hipSuccess)
-            return FDF_ERR_DEVICE;
-    }
-    if (++ctx->epoch > 0xffffu) {   // generation tag wrapped: clear stale look-back words
-        ctx->epoch = 1;
-        if (hipMemsetAsync(ctx->d_state, 0, ctx->state_n * sizeof(unsigned long long), stream) !=
-            hipSuccess)
-            return FDF_ERR_DEVICE;
-    }
     const char* dbg = std::getenv("FDF_DEBUG_FLAGS");   // ablation runs only, see fdf_kernels.h
     fdfk::BandParams p;
     p.frames = d_frames;
@@ -194,14 +177,11 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.words_per_row = nw;
     c.slot_bytes = slot_bytes;
     c.tasks_per_group = tpg;
-    c.epoch = ctx->epoch;
     c.slots = ctx->d_slots;
     c.counts = ctx->d_counts;
     c.out = d_out;
     c.cap = cap;
     c.frame_offsets = d_offsets;
-    c.state = ctx->d_state;
-    c.ticket = ctx->d_ticket;
     hipEvent_t* ev = nullptr;
     if (ctx->timing && ctx->timed < kMaxTimedCalls) {
         while (ctx->ev.size() < 3 * (ctx->timed + 1)) {
@@ -380,8 +360,6 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_map);
-        (void)hipFree(ctx->d_state);
-        (void)hipFree(ctx->d_ticket);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(ctx->stream);
     }

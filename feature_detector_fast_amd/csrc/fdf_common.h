@@ -144,9 +144,4 @@ __device__ __forceinline__ uint32_t score_sum_abs(uint32_t c, const uint32_t (&p
     return max(sb, sd);
 }
 
-__device__ __forceinline__ unsigned long long lb_pack(uint32_t epoch, uint32_t flag,
-                                                      unsigned long long value) {
-    return ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | value;
-}
-
 }  // namespace fdfk

@@ -36,6 +36,11 @@ constexpr uint32_t kSweepMaxLds = 160 * 1024; // gfx950 LDS per CU (and per work
 #define FDF_ISSUE 3
 #endif
 constexpr int kSweepIssue = FDF_ISSUE;
+// Full-test batches in flight (each evaluated kSweepBatchSlots issue points after its issue).
+#ifndef FDF_BATCH_SLOTS
+#define FDF_BATCH_SLOTS 1
+#endif
+constexpr int kSweepBatchSlots = FDF_BATCH_SLOTS;
 // Pixel-row register ring of the sweep (rows in flight = kSweepRing - 4); unit sweeps are
 // whole multiples of kSweepRing steps.
 #ifndef FDF_RING
@@ -126,14 +131,11 @@ __host__ __device__ inline uint32_t compact_tasks_per_group(uint32_t ntasks) {
 struct CompactParams {
     uint32_t width, height, rows, bands_per_frame, ntasks, words_per_row, slot_bytes;
     uint32_t tasks_per_group;        // compact_tasks_per_group(ntasks)
-    uint32_t epoch;                  // look-back generation tag, 1..65535
     const uint8_t* slots;
     const uint32_t* counts;
     uint2* out;
     uint64_t cap;
     uint64_t* frame_offsets;         // frames + 1 entries
-    unsigned long long* state;       // >= ceil(ntasks / tasks_per_group) look-back words
-    uint32_t* ticket;                // zero between launches (self-resetting)
 };
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);

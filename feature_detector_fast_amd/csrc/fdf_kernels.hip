@@ -2,8 +2,8 @@
 //
 // compact_kernel -- turns the detector's per-band slots into the reference's output: one
 //   list of points per frame, in raster order (src/fast_simd.rs:589-616 pushes keypoints in
-//   scan order).  Band counts are scanned in raster order with a decoupled look-back over
-//   groups of bands, then each group copies its bands' points to their final positions.
+//   scan order).  Each group of bands sums the counts of the bands before it (all final
+//   when the kernel starts), then copies its bands' points to their final positions.
 // score_points_kernel -- the reference's two NMS score functions on given points
 //   (extension: fdf_score_points).
 // rgb_to_luma_kernel -- RGB8 -> grey exactly as image 0.24.6's to_luma8, which the
@@ -51,19 +51,11 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
     __shared__ uint32_t s_task_off[kCompactTasks + 1];
     __shared__ uint32_t s_list_off[kCompactTasks + 1];
     __shared__ uint32_t s_wave_sum[kCompactTasks / 64];
-    __shared__ unsigned long long s_base;
-    __shared__ uint32_t s_group;
+    __shared__ unsigned long long s_part[kCompactTasks / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t T = P.tasks_per_group;
-    const uint32_t ngroups = (P.ntasks + T - 1) / T;
-    if (tid == 0) {   // groups in dispatch order: a group's predecessors are resident or done
-        const uint32_t g = atomicAdd(P.ticket, 1u);
-        if (g == ngroups - 1) atomicExch(P.ticket, 0u);
-        s_group = g;
-    }
-    __syncthreads();
-    const uint32_t g = s_group;
+    const uint32_t g = blockIdx.x;
     const uint32_t first = g * T;
     const uint32_t ntask_here = min(T, P.ntasks - first);
     const uint32_t task = first + tid;
@@ -81,50 +73,18 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
         s_list_off[kCompactTasks] = list_total;
     }
 
-    // decoupled look-back: wave 0 probes 64 predecessor groups per round
-    if (wave == 0) {
-        unsigned long long excl = 0;
-        if (g == 0) {
-            if (lane == 0)
-                __hip_atomic_store(&P.state[0], lb_pack(P.epoch, 2, total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0)
-                __hip_atomic_store(&P.state[g], lb_pack(P.epoch, 1, total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            int64_t top = (int64_t)g - 1;
-            while (true) {
-                const int64_t idx = top - (int64_t)lane;
-                uint32_t flag = 2;                                   // before group 0: 0 incl.
-                unsigned long long val = 0;
-                if (idx >= 0) {
-                    const unsigned long long wv = __hip_atomic_load(
-                        &P.state[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    flag = (uint32_t)(wv >> 48) == P.epoch ? (uint32_t)(wv >> 46) & 3u : 0u;
-                    val = wv & ((1ull << 46) - 1);
-                }
-                const uint64_t inc = wave_ballot(flag == 2);
-                const uint64_t missing = wave_ballot(flag == 0);
-                const uint64_t upto = inc ? (inc & (~inc + 1)) * 2 - 1 : ~0ull;
-                if (missing & upto) {
-                    __builtin_amdgcn_s_sleep(2);
-                    continue;
-                }
-                unsigned long long part = ((upto >> lane) & 1) ? val : 0ull;
+    // the group's base: every band count is final when this kernel starts (the detector
+    // kernel wrote them), so each group sums its predecessors' counts itself -- a few KB of
+    // L2-resident reads, no cross-group hand-off
+    unsigned long long part = 0;
+    for (uint32_t i = tid; i < first; i += kCompactTasks) part += P.counts[i];
 #pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
-                excl += part;
-                if (inc) break;
-                top -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(&P.state[g], lb_pack(P.epoch, 2, excl + total),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) s_base = excl;
-    }
+    for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
+    if (lane == 0) s_part[wave] = part;
     __syncthreads();
-    const unsigned long long base = s_base;
+    unsigned long long base = 0;
+#pragma unroll
+    for (int w = 0; w < kCompactTasks / 64; ++w) base += s_part[w];
     if (mine) {
         const uint32_t frame = task / P.bands_per_frame;
         const uint32_t band = task - frame * P.bands_per_frame;

@@ -255,11 +255,14 @@ __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>:
 // Test everything queued, now (FIFO overflow, the end of a unit).
 template <int NMS, int N, int LC>
 __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
-                                            const LerpConsts& lk, bool& inflight,
-                                            const Batch& batch) {
-    if (inflight) {
-        evaluate_batch<NMS, N, LC>(sh, u, lk, batch);
-        inflight = false;
+                                            const LerpConsts& lk, bool (&inflight)[kSweepBatchSlots],
+                                            const Batch (&batch)[kSweepBatchSlots]) {
+#pragma unroll
+    for (int q = 0; q < kSweepBatchSlots; ++q) {
+        if (inflight[q]) {
+            evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);
+            inflight[q] = false;
+        }
     }
     while (u.tail != u.head) {
         if (u.flags & kFlagNoFullTest) {
@@ -296,8 +299,12 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
     u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
     u.head = u.tail = 0;
-    bool inflight = false;
-    Batch batch;
+    // kSweepBatchSlots batches in flight, in static slots (issue point q of the K-step loop
+    // body uses slot q % slots), each evaluated slots issue points after it was issued
+    bool inflight[kSweepBatchSlots];
+    Batch batch[kSweepBatchSlots];
+#pragma unroll
+    for (int q = 0; q < kSweepBatchSlots; ++q) inflight[q] = false;
 
     // One kSweepRing-slot ring of pixel rows: row r in slot (r - ys) % kSweepRing.  At step J
     // (row yv) it holds rows yv .. yv+K-2 (K = kSweepRing) with yv+4 .. yv+K-2 still loading,
@@ -368,21 +375,24 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             }                                                                                \
         }                                                                                    \
         if (((J) % kIssue) == kIssue - 1) {                                                  \
-            /* the batch issued kIssue rows ago is due; issue the next full one */           \
-            if (inflight) {                                                                  \
-                evaluate_batch<NMS, N, LC>(sh, u, lk, batch);                                \
-                inflight = false;                                                            \
+            /* the batch of this slot is due; issue the next full one into it */             \
+            constexpr int q = ((J) / kIssue) % kSweepBatchSlots;                             \
+            if (inflight[q]) {                                                               \
+                evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);                             \
+                inflight[q] = false;                                                         \
             }                                                                                \
             const uint32_t pend = u.tail - u.head;                                           \
             const bool go = pend >= 64;                                                      \
             if (go && (u.flags & kFlagNoFullTest)) u.head += 64u;                            \
             const uint32_t n = (go && !(u.flags & kFlagNoFullTest)) ? 64u : 0u;              \
-            batch = issue_batch<LC>(sh, u, n);                                               \
-            inflight = n != 0;                                                               \
+            batch[q] = issue_batch<LC>(sh, u, n);                                            \
+            inflight[q] = n != 0;                                                            \
         }                                                                                    \
     }
 
     static_assert(K == 8 || K == 12 || K == 16, "ring of 8, 12 or 16 rows");
+    static_assert((K / kIssue) % kSweepBatchSlots == 0 || kSweepBatchSlots == 1,
+                  "issue points per loop body must cycle through the batch slots");
     for (int i0 = 0; i0 < T; i0 += K) {
         FDF_SWEEP_STEP(0)
         FDF_SWEEP_STEP(1)

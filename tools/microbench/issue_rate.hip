@@ -39,6 +39,11 @@ KERNEL(k_or3, BODY8_3("v_or3_b32"))
 KERNEL(k_add3, BODY8_3("v_add3_u32"))
 KERNEL(k_sad, BODY8_3("v_sad_u8"))
 KERNEL(k_max3, BODY8_3("v_max3_u32"))
+KERNEL(k_bitop3, asm volatile("v_bitop3_b32 %0, %0, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %2, %2, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %3, %3, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %4, %4, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %5, %5, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %6, %6, %8, %8 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %8, %8 bitop3:0x96" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b)))
+KERNEL(k_xor, BODY8("v_xor_b32"))
+KERNEL(k_not, asm volatile("v_not_b32 %0, %0\n\tv_not_b32 %1, %1\n\tv_not_b32 %2, %2\n\tv_not_b32 %3, %3\n\tv_not_b32 %4, %4\n\tv_not_b32 %5, %5\n\tv_not_b32 %6, %6\n\tv_not_b32 %7, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b)))
+KERNEL(k_and_or, BODY8_3("v_and_or_b32"))
+KERNEL(k_lshr, BODY8("v_lshrrev_b32"))
 
 typedef void (*Fn)(uint32_t*, uint32_t);
 double run(Fn f) {
@@ -66,7 +71,8 @@ int main() {
         {"v_pk_add_u16", k_pkadd}, {"v_pk_max_u16", k_pkmax}, {"v_lerp_u8", k_lerp},
         {"v_alignbyte_b32", k_align}, {"v_perm_b32", k_perm}, {"v_bfi_b32", k_bfi},
         {"v_or3_b32", k_or3}, {"v_add3_u32", k_add3}, {"v_sad_u8", k_sad},
-        {"v_max3_u32", k_max3}};
+        {"v_max3_u32", k_max3}, {"v_bitop3_b32", k_bitop3}, {"v_xor_b32", k_xor},
+        {"v_not_b32", k_not}, {"v_and_or_b32", k_and_or}, {"v_lshrrev_b32", k_lshr}};
     for (auto& k : ks) {
         const double r = run(k.f);
         printf("%-16s %7.1f G wave-instr/s  %.3f per CU-cycle @2.4GHz\n", k.n, r, r / 256 / 2.4);
