@@ -22,6 +22,7 @@ constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (count
 constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compaction only)
 constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
 constexpr uint32_t kFlagNoNms = 16;       // NMS modes: every keypoint is kept (no band NMS pass)
+constexpr uint32_t kFlagNmsPrefixOnly = 32;  // band NMS pass: rank prefixes only (timing)
 
 // Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).
@@ -58,13 +59,15 @@ constexpr int kSweepWavesPerEU = FDF_WAVES_PER_EU;
 __host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 0u; }
 
 // LDS of one workgroup: 4 candidate FIFOs and the keypoint bitmap of the band's R rows plus
-// the NMS halo rows (NMS then clears the suppressed keypoints in place).  NMS also keeps the
-// band's keypoint scores: a list of kScoreListCap (position, score) entries, the scores
-// scattered into raster rank order, and per-row / per-8-word-block keypoint counts that
-// turn a bitmap position into its rank.
+// the NMS halo rows (NMS then clears the suppressed keypoints in place; one pad word after
+// the bitmap lets bit look-ups read two words unconditionally).  NMS also keeps the band's
+// keypoint scores: a list of kScoreListCap (position, score) entries and per-row /
+// per-4-word-block keypoint counts that turn a bitmap position into its raster rank; the
+// scores in rank order go to the FIFO area once the sweep is done.
 constexpr uint32_t kScoreListCap = 2048;
+constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix block
 struct SweepLayout {
-    uint32_t pq, wave_bytes, bitmap, slist, sranked, bprefix, rprefix, misc, total;
+    uint32_t pq, wave_bytes, bitmap, slist, bprefix, rprefix, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t v);
@@ -72,14 +75,13 @@ __host__ __device__ inline uint32_t align16(uint32_t v);
 __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw, uint32_t nms) {
     SweepLayout L;
     const uint32_t rows = R + 2 * band_halo(nms);
-    const uint32_t nb = (nw + 7) / 8;
+    const uint32_t nb = (nw + kRankBlock - 1) / kRankBlock;
     L.pq = 0;
-    L.wave_bytes = kSweepPixelQ * 4;
+    L.wave_bytes = kSweepPixelQ * 4;              // 4 FIFOs = kScoreListCap u16 ranked scores
     L.bitmap = 4 * L.wave_bytes;
-    L.slist = L.bitmap + align16(rows * nw * 4);
+    L.slist = L.bitmap + align16(rows * nw * 4 + 4);
     const uint32_t cap = nms ? kScoreListCap : 0u;
-    L.sranked = L.slist + cap * 4;
-    L.bprefix = L.sranked + cap * 2;
+    L.bprefix = L.slist + cap * 4;
     L.rprefix = L.bprefix + (nms ? align16(rows * nb * 2) : 0u);
     L.misc = L.rprefix + (nms ? align16(rows * 4) : 0u);
     L.total = L.misc + 64;

@@ -207,8 +207,12 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
                 uint32_t p[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+#ifdef FDF_ABLATE_NO_SCORE   // timing ablation only: wrong NMS results
+                const uint32_t score = 1u + (p[0] & 1u);
+#else
                 const uint32_t score = NMS == kNmsMaxThreshold ? score_max_threshold<N>(c, p, kd)
                                                                : score_sum_abs(c, p, u.t);
+#endif
                 const uint32_t idx = base + lanes_below(bal);
                 if (idx < sh.slist_cap) {
                     sh.slist[idx] = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
@@ -419,12 +423,12 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
-// Three bitmap bits of one bitmap row: columns x-1, x, x+1 (x-1 >= 2, x+1 < W - 3).
+// Three bitmap bits of one bitmap row: columns x-1, x, x+1 (x-1 >= 2, x+1 < W - 3).  Both
+// words are read unconditionally (the bitmap has a pad word after its last row).
 __device__ __forceinline__ uint32_t bits3(const uint32_t* row, int x) {
     const int xm = x - 1, wi = xm >> 5, sh = xm & 31;
-    uint32_t v = row[wi] >> sh;
-    if (sh > 29) v |= row[wi + 1] << (32 - sh);
-    return v & 7u;
+    const uint64_t v = ((uint64_t)row[wi + 1] << 32) | row[wi];
+    return (uint32_t)(v >> sh) & 7u;
 }
 
 // Strict 3x3 maximum of one keypoint (src/fast_simd.rs:596-615): keep iff its score is above
@@ -597,23 +601,27 @@ __device__ void band_nms(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t 
     }
     __syncthreads();
     // rows 3 and h - 4 keep no keypoints (they were neighbours only)
-    for (uint32_t r = 0; r < rows; ++r) {
-        const uint32_t y = y0 + r;
-        if (y != 3 && y != H - 4) continue;
-        for (uint32_t w = tid; w < nw; w += kThreads) bitmap[(r + 1) * nw + w] = 0;
+    for (uint32_t y : {3u, H - 4u}) {
+        if (y < y0 || y >= y0 + rows) continue;
+        for (uint32_t w = tid; w < nw; w += kThreads) bitmap[(y - y0 + 1) * nw + w] = 0;
     }
     __syncthreads();
 }
 
 // Raster rank of bitmap position (row, x): keypoints before it in the band's bitmap.
-// rprefix[row] counts the rows above, bprefix[row * nb + k] the words [0, 8k) of the row.
+// rprefix[row] counts the rows above, bprefix[row * nb + k] the words [0, 4k) of the row.
 __device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const uint16_t* bprefix,
                                                 const uint32_t* rprefix, uint32_t nw, uint32_t nb,
                                                 uint32_t row, uint32_t x) {
-    const uint32_t wi = x >> 5, blk = wi >> 3;
+    static_assert(kRankBlock == 4, "three block words before the position's word");
+    const uint32_t wi = x >> 5, blk = wi / kRankBlock, w0 = blk * kRankBlock;
     const uint32_t* rw = bitmap + row * nw;
     uint32_t r = rprefix[row] + bprefix[row * nb + blk];
-    for (uint32_t j = 8 * blk; j < wi; ++j) r += __popc(rw[j]);
+#pragma unroll
+    for (uint32_t j = 0; j < kRankBlock - 1; ++j) {
+        const uint32_t v = rw[min(w0 + j, wi)];         // in-row, read unconditionally
+        r += w0 + j < wi ? __popc(v) : 0u;
+    }
     return r + __popc(rw[wi] & ((1u << (x & 31)) - 1u));
 }
 
@@ -626,25 +634,49 @@ __device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const ui
 template <int NMS>
 __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
                              uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
-                             uint16_t* bprefix, uint32_t* rprefix) {
+                             uint16_t* bprefix, uint32_t* rprefix, uint32_t flags) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t R2 = rows + 2, nb = (nw + 7) / 8;
-    for (uint32_t i = tid; i < R2 * nb; i += kThreads) {
-        const uint32_t row = i / nb, k = i - row * nb;
-        const uint32_t* rw = bitmap + row * nw;
-        uint32_t cnt = 0;
-        for (uint32_t j = 8 * k; j < min(8 * k + 8, nw); ++j) cnt += __popc(rw[j]);
-        bprefix[i] = (uint16_t)cnt;
-    }
-    __syncthreads();
-    for (uint32_t row = tid; row < R2; row += kThreads) {
-        uint32_t acc = 0;
-        for (uint32_t k = 0; k < nb; ++k) {
-            const uint32_t c = bprefix[row * nb + k];
-            bprefix[row * nb + k] = (uint16_t)acc;
-            acc += c;
+    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    if (nb_blocks <= 16) {
+        // one bitmap row per 16-lane DPP row: lane k counts block k, a row_shr scan turns the
+        // counts into the row's block prefixes and lane 15 ends with the row total
+        for (uint32_t base = 0; base < R2; base += kThreads / 16) {
+            const uint32_t row = base + tid / 16, k = tid & 15u;
+            const bool act = row < R2 && k < nb_blocks;
+            uint32_t cnt = 0;
+            if (act) {
+                const uint32_t* rw = bitmap + row * nw;
+#pragma unroll
+                for (uint32_t j = 0; j < kRankBlock; ++j)
+                    cnt += kRankBlock * k + j < nw ? __popc(rw[kRankBlock * k + j]) : 0u;
+            }
+            uint32_t inc = cnt;
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xf, 0xf, false);   // row_shr:1
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xf, 0xf, false);   // row_shr:2
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xf, 0xf, false);   // row_shr:4
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xf, 0xf, false);   // row_shr:8
+            if (act) bprefix[row * nb_blocks + k] = (uint16_t)(inc - cnt);
+            if (row < R2 && k == 15u) rprefix[row] = inc;
         }
-        rprefix[row] = acc;
+    } else {
+        for (uint32_t i = tid; i < R2 * nb_blocks; i += kThreads) {
+            const uint32_t row = i / nb_blocks, k = i - row * nb_blocks;
+            const uint32_t* rw = bitmap + row * nw;
+            uint32_t cnt = 0;
+            for (uint32_t j = kRankBlock * k; j < min(kRankBlock * k + kRankBlock, nw); ++j)
+                cnt += __popc(rw[j]);
+            bprefix[i] = (uint16_t)cnt;
+        }
+        __syncthreads();
+        for (uint32_t row = tid; row < R2; row += kThreads) {
+            uint32_t acc = 0;
+            for (uint32_t k = 0; k < nb_blocks; ++k) {
+                const uint32_t c = bprefix[row * nb_blocks + k];
+                bprefix[row * nb_blocks + k] = (uint16_t)acc;
+                acc += c;
+            }
+            rprefix[row] = acc;
+        }
     }
     __syncthreads();
     if (tid < 64) {   // exclusive scan of the row totals
@@ -662,9 +694,16 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
         }
     }
     __syncthreads();
+    if (flags & kFlagNmsPrefixOnly) return;
+    // scores of keypoints with a neighbouring keypoint into rank order (the others' scores are
+    // never read: an isolated keypoint is kept, and marked by a zero score field)
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
-        sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb, row, x)] = (uint16_t)(e & 0xfffu);
+        const uint32_t nb = bits3(bitmap + (row - 1 + (row == 0)) * nw, (int)x) * (row != 0) |
+                            (bits3(bitmap + row * nw, (int)x) & 5u) |
+                            (row + 1 < R2 ? bits3(bitmap + (row + 1) * nw, (int)x) : 0u);
+        if (nb == 0) slist[i] = e & ~0xfffu;
+        else sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
     }
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) {
@@ -672,34 +711,37 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
         if (row == 0 || row == R2 - 1) continue;          // rows outside the band
         const uint32_t y = y0 - 1 + row;
         const uint32_t own = e & 0xfffu;
-        uint32_t mx = 0;
-        const uint32_t mid = bits3(bitmap + row * nw, (int)x);
-        if (mid & 5u) {
-            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb, row, x);
-            if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
-            if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
-        }
+        bool suppressed = y == 3 || y == H - 4;
+        if (own != 0 && !suppressed) {
+            uint32_t mx = 0;
+            const uint32_t mid = bits3(bitmap + row * nw, (int)x);
+            if (mid & 5u) {
+                const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+                if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
+                if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
+            }
 #pragma unroll
-        for (int d = -1; d <= 1; d += 2) {
-            const uint32_t nbits = bits3(bitmap + (row + d) * nw, (int)x);
-            if (nbits) {
-                uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb, row + d, x - 1);
+            for (int d = -1; d <= 1; d += 2) {
+                const uint32_t nbits = bits3(bitmap + (row + d) * nw, (int)x);
+                if (nbits) {
+                    uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    if ((nbits >> k) & 1u) {
-                        mx = max(mx, (uint32_t)sranked[r]);
-                        ++r;
+                    for (int k = 0; k < 3; ++k) {
+                        if ((nbits >> k) & 1u) {
+                            mx = max(mx, (uint32_t)sranked[r]);
+                            ++r;
+                        }
                     }
                 }
             }
+            suppressed = own <= mx;
         }
-        const bool suppressed = own <= mx || y == 3 || y == H - 4;
         slist[i] = (e & ~0xfffu) | (suppressed ? 1u : 0u);
     }
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i];
-        if (e & 1u) {
+        if ((e & 0xfffu) == 1u) {
             const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
             atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
         }
@@ -738,7 +780,7 @@ void fast_sweep_kernel(BandParams P) {
         return;
     }
     uint32_t* unit_ctr = wave_sum + kWaves;
-    for (uint32_t i = tid; i < (rows + 2 * halo) * nw; i += kThreads) bitmap[i] = 0;
+    for (uint32_t i = tid; i <= (rows + 2 * halo) * nw; i += kThreads) bitmap[i] = 0;   // + pad
     if (tid == 0) {
         unit_ctr[0] = 0;
         unit_ctr[1] = 0;
@@ -812,9 +854,9 @@ void fast_sweep_kernel(BandParams P) {
         if (P.flags & kFlagNoNms) {
         } else if (n <= sh.slist_cap) {
             band_nms_lds<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, n,
-                              reinterpret_cast<uint16_t*>(smem_raw + L.sranked),
+                              reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                               reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix));
+                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), P.flags);
         } else {
             // more keypoints than the list holds: the listed scores join the score map
             for (uint32_t i = tid; i < sh.slist_cap; i += kThreads) {
