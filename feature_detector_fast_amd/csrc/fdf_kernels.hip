@@ -77,7 +77,16 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
     // kernel wrote them), so each group sums its predecessors' counts itself -- a few KB of
     // L2-resident reads, no cross-group hand-off
     unsigned long long part = 0;
-    for (uint32_t i = tid; i < first; i += kCompactTasks) part += P.counts[i];
+    {   // 16-byte loads, several in flight per thread (P.counts is 16-byte aligned)
+        const uint4* c4 = reinterpret_cast<const uint4*>(P.counts);
+        const uint32_t n4 = first / 4;
+#pragma unroll 4
+        for (uint32_t i = tid; i < n4; i += kCompactTasks) {
+            const uint4 v = c4[i];
+            part += (unsigned long long)v.x + v.y + v.z + v.w;
+        }
+        for (uint32_t i = 4 * n4 + tid; i < first; i += kCompactTasks) part += P.counts[i];
+    }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
     if (lane == 0) s_part[wave] = part;
