@@ -763,11 +763,31 @@ void fast_sweep_kernel(BandParams P) {
     const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
     constexpr uint32_t halo = NMS == kNmsOff ? 0u : 1u;
 
-    // XCD-aware static task mapping: consecutive bands of a frame land on one XCD (its L2
-    // then serves the halo rows two neighbouring bands share)
+    // XCD-aware static task mapping: each XCD takes a contiguous range of bands (raster
+    // order), so consecutive bands of a frame land on one XCD (its L2 then serves the halo
+    // rows two neighbouring bands share).  Within its range an XCD dispatches the frames'
+    // full bands first and their (shorter) last bands at the end, where they fill the grid's
+    // tail.
     const uint32_t b = blockIdx.x;
     const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
-    const uint32_t task = k8 * q8 + min(k8, r8) + (b >> 3);
+    const uint32_t c0 = k8 * q8 + min(k8, r8), j = b >> 3;
+    uint32_t task = c0 + j;
+#ifndef FDF_RASTER_DISPATCH
+    {
+        const uint32_t c1 = c0 + q8 + (k8 < r8 ? 1u : 0u);
+        const uint32_t B = P.bands_per_frame;
+        if (B > 1) {
+            const uint32_t s0 = c0 / B, s1 = c1 / B;          // last bands before c0 / c1
+            const uint32_t n_full = (c1 - c0) - (s1 - s0);
+            if (j < n_full) {
+                const uint32_t u = (c0 - s0) + j;              // index among full bands
+                task = (u / (B - 1)) * B + u % (B - 1);
+            } else {
+                task = (s0 + (j - n_full)) * B + (B - 1);
+            }
+        }
+    }
+#endif
     const uint32_t frame = task / P.bands_per_frame;
     const uint32_t band = task - frame * P.bands_per_frame;
     const uint32_t y0 = 3 + band * P.rows;
