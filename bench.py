@@ -123,6 +123,41 @@ def cpu_baseline(args, nms):
     return base, mt
 
 
+def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, device,
+               frames=128, steps=10):
+    """BASELINE.json config 5 on this GPU: 3840x2160 S1 frames, t=8 n=12 (3-of-4 cardinal
+    pre-filter), SAD NMS; 128 frames = 1.06 GB, the same bytes per launch as config 4."""
+    import torch
+
+    W, H = 3840, 2160
+    batch = workloads.s1_frames_torch(0, frames, W, H, device=device)
+    offs = torch.zeros(frames + 1, dtype=torch.int64, device=device)
+    cfg = Config(8, 12, NonMaximalSuppression.SumAbsolute)
+    for _ in range(3):
+        fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
+    ctx = fast_hip.context(device.index or 0)
+    ctx.set_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    calls, sweep_ms, compact_ms = ctx.timing()
+    ctx.set_timing(False)
+    kernel_ms = sweep_ms / max(calls, 1)
+    alg = frames * W * H
+    res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad",
+           "Mpix_s": round(alg * steps / elapsed / 1e6, 1),
+           "ms_per_step": round(elapsed * 1e3 / steps, 4),
+           "kernel_ms_avg": round(kernel_ms, 4),
+           "compaction_kernel_ms_avg": round(compact_ms / max(calls, 1), 4),
+           "roofline_frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "keypoints_per_step": int(offs[-1].item())}
+    del batch
+    return res
+
+
 def main(argv=None):
     args = parse_args(argv)
     world, rank, local = dist_env()
@@ -234,6 +269,8 @@ def main(argv=None):
             extras[f"single_frame_{name}_ms_p50"] = round(lat[len(lat) // 2], 4)
             extras[f"single_frame_{name}_Mpix_s"] = round(W * H / (lat[len(lat) // 2] * 1e-3) / 1e6, 1)
             extras[f"single_frame_{name}_kp"] = int(offs[1].item())
+        extras["config5_4k"] = config5_4k(fast_hip, Config, NonMaximalSuppression, workloads,
+                                          out, stream, device)
         if world == 1 and args.cpu_seconds > 0:
             cpu, cpu_mt = cpu_baseline(args, nms)
             extras["cpu_baseline_all_cores"] = cpu_mt

@@ -144,7 +144,9 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     const uint64_t ntasks = (uint64_t)bands * n_frames;
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
     const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw);
-    const uint32_t tpg = fdfk::compact_tasks_per_group((uint32_t)ntasks);
+    uint32_t tpg = fdfk::compact_tasks_per_group((uint32_t)ntasks);
+    if (const char* e = std::getenv("FDF_COMPACT_TPG"))   // ablation runs only
+        tpg = std::max(1u, std::min((uint32_t)fdfk::kCompactTasks, (uint32_t)std::strtoul(e, nullptr, 0)));
     int rc;
     if ((rc = ensure(&ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), false, stream))) return rc;
     if ((rc = ensure(&ctx->d_counts, &ctx->counts_n, (size_t)ntasks, false, stream))) return rc;

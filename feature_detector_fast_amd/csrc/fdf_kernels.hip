@@ -103,16 +103,30 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
 
     // slot lists: output k of the group's listed points -> band i with
     // s_list_off[i] <= k < s_list_off[i + 1] (bands with bitmaps add nothing to that prefix)
-    for (uint32_t k = tid; k < list_total; k += kCompactTasks) {
-        uint32_t lo = 0, hi = ntask_here;                    // invariant: off[lo] <= k < off[hi]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_list_off[mid] <= k) lo = mid; else hi = mid;
+    // (kCopyUnroll points per thread per round, their loads in flight together)
+    constexpr int kCopyUnroll = 4;
+    for (uint32_t k0 = tid; k0 < list_total; k0 += kCopyUnroll * kCompactTasks) {
+        uint2 v[kCopyUnroll];
+        unsigned long long o[kCopyUnroll];
+#pragma unroll
+        for (int q = 0; q < kCopyUnroll; ++q) {
+            const uint32_t k = k0 + q * kCompactTasks;
+            o[q] = ~0ull;
+            v[q] = make_uint2(0u, 0u);
+            if (k < list_total) {
+                uint32_t lo = 0, hi = ntask_here;            // invariant: off[lo] <= k < off[hi]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_list_off[mid] <= k) lo = mid; else hi = mid;
+                }
+                const uint32_t j = k - s_list_off[lo];
+                o[q] = base + s_task_off[lo] + j;
+                v[q] = reinterpret_cast<const uint2*>(P.slots + (uint64_t)(first + lo) * P.slot_bytes)[j];
+            }
         }
-        const uint32_t j = k - s_list_off[lo];
-        const unsigned long long o = base + s_task_off[lo] + j;
-        const uint2* src = reinterpret_cast<const uint2*>(P.slots + (uint64_t)(first + lo) * P.slot_bytes);
-        if (o < P.cap) P.out[o] = src[j];
+#pragma unroll
+        for (int q = 0; q < kCopyUnroll; ++q)
+            if (o[q] < P.cap) P.out[o[q]] = v[q];
     }
 
     // bitmap bands: one wave each, 64 words per round, in raster order
