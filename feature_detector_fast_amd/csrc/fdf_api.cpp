@@ -104,9 +104,9 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) 
     // extra rows a unit tests: NMS bands test one row above and below (first / last unit)
     const uint32_t halo = fdfk::band_halo(nms) * (g.nsub == 1 ? 2u : 1u);
     // LDS per workgroup sets the workgroups per CU: <= 40 KB keeps 4.
-    // Without NMS a 34 KB budget (bands of ~122 rows at 1080p) measured faster than the
+    // Without NMS a 35 KB budget (bands of ~122 rows at 1080p) measured faster than the
     // tallest band that fits (more, shorter workgroups: a shorter grid tail).
-    uint32_t budget = nms ? 40000u : 34000u;
+    uint32_t budget = nms ? 40000u : 35000u;
     if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the

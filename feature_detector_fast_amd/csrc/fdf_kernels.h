@@ -58,7 +58,7 @@ constexpr int kSweepWavesPerEU = FDF_WAVES_PER_EU;
 // neighbouring bands' rows, so the band also tests one row each side (scores only).
 __host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 0u; }
 
-// LDS of one workgroup: 4 candidate FIFOs and the keypoint bitmap of the band's R rows plus
+// LDS of one workgroup: 4 candidate FIFOs (+ batch staging) and the keypoint bitmap of the band's R rows plus
 // the NMS halo rows (NMS then clears the suppressed keypoints in place; one pad word after
 // the bitmap lets bit look-ups read two words unconditionally).  NMS also keeps the band's
 // keypoint scores: a list of kScoreListCap (position, score) entries and per-row /
@@ -67,7 +67,7 @@ __host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 
 constexpr uint32_t kScoreListCap = 2048;
 constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix block
 struct SweepLayout {
-    uint32_t pq, wave_bytes, bitmap, slist, bprefix, rprefix, misc, total;
+    uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t v);
@@ -78,7 +78,8 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     const uint32_t nb = (nw + kRankBlock - 1) / kRankBlock;
     L.pq = 0;
     L.wave_bytes = kSweepPixelQ * 4;              // 4 FIFOs = kScoreListCap u16 ranked scores
-    L.bitmap = 4 * L.wave_bytes;
+    L.stage = 4 * L.wave_bytes;                   // 4 x 64 staged batch pixels
+    L.bitmap = L.stage + 4 * 64 * 4;
     L.slist = L.bitmap + align16(rows * nw * 4 + 4);
     const uint32_t cap = nms ? kScoreListCap : 0u;
     L.bprefix = L.slist + cap * 4;

@@ -98,7 +98,9 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
 }
 
 struct SweepShared {
-    uint32_t* pq;          // kSweepPixelQ FIFO of (row << 11) | (lane << 5) | flag bit
+    uint32_t* pq;          // kSweepPixelQ FIFO of lane rows with candidates: (row - ys) << 22 |
+                           // lane << 16 | 16-bit mask (bit b = lane column 4 (b & 3) + (b >> 2))
+    uint32_t* stage;       // 64 pixels of the batch being issued: (row - ys) << 10 | strip column
     uint32_t* bitmap;      // band keypoints: bitmap row i = image row yb + i, words_per_row each
     uint32_t* slist;       // NMS: the band's keypoints as (bitmap row * W + x) << 12 | score
     uint32_t* slist_n;     // entries appended (past slist_cap: the rest went to the map)
@@ -113,6 +115,7 @@ struct UnitCtx {
     int yb;                // image row of bitmap row 0 (band start minus the NMS halo)
     uint32_t lane;
     uint32_t head, tail;   // candidate FIFO: entries [head, tail) at pq[i % kSweepPixelQ]
+    int ys;                // first row the unit sweeps (FIFO rows are relative to it)
     uint32_t flags;        // BandParams::flags (ablation runs only)
     uint8_t* smap;         // NMS: this frame's score map
 };
@@ -124,35 +127,88 @@ struct UnitCtx {
 // ---------------------------------------------------------------------------------------
 struct Batch {
     uint32_t code;         // (row << 10) | strip column
+    uint32_t n;            // pixels in the batch (wave-uniform)
     bool act;
     uint32_t a0, a6;       // rows y-3, y+3: 4 bytes from x-1
     u32x2 a1, a5;          // rows y-2, y+2: 8 bytes from x-2
     u32x2 a2, a3, a4;      // rows y-1, y, y+1: 8 bytes from x-3
 };
 
-// Pops n (<= 64) entries.  n = 0 still issues the loads (all lanes at a harmless address):
-// the pipelined issue points load unconditionally, so that every path through the sweep
-// has the same sequence of loads and the compiler's vmcnt counts stay exact.
+// Inclusive prefix sum over the wave's 64 lanes (DPP row shifts, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+
+// Pops the next 64 candidate pixels (fewer only when `force`: a flush) and starts their
+// loads.  The FIFO holds lane rows; the pixels of the first 64 entries are counted with a
+// wave prefix sum, every contributing entry writes its pixels to the staging array in
+// order, and an entry only partly taken keeps its other pixels at the FIFO head.  Without
+// a batch the loads are still issued (all lanes at a harmless address): the pipelined issue
+// points load unconditionally, so that every path through the sweep has the same sequence
+// of loads and the compiler's vmcnt counts stay exact.
+// The FIFO entries a batch is built from: read early (the issue step's first instruction)
+// so the LDS latency hides behind the step's pre-filter work.
+struct FifoPeek {
+    uint32_t nent;         // entries read (wave-uniform)
+    uint32_t e;            // this lane's entry (0 past nent)
+};
+__device__ __forceinline__ FifoPeek fifo_peek(const SweepShared& sh, const UnitCtx& u) {
+    FifoPeek f;
+    f.nent = min(u.tail - u.head, 64u);
+    f.e = u.lane < f.nent ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
+    return f;
+}
+
 template <int LC>
-__device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, uint32_t n) {
+__device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, bool force,
+                                             const FifoPeek& pk) {
+    static_assert(LC == 16, "16-bit lane masks");
     Batch b;
-    b.act = u.lane < n;
-    const int W = (int)u.src.W;
-    // inactive lanes read around centre (3, 3), which every tested frame has; an empty batch
-    // (n = 0, wave-uniform) skips the FIFO read and the decoding
-    int o = 3 * W + 3 - 3 * W;                                  // pixel (x, y - 3) of (3, 3)
+    b.n = 0;
+    b.act = false;
     b.code = 0;
-    if (n != 0) {
-        // FIFO entry (row << 11) | (lane << 5) | bit, bit 8j + m = lane column 4m + j  ->
-        // the test's code (row << 10) | strip column
-        const uint32_t e = b.act ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
-        const uint32_t bit = e & 31u;
-        b.code = ((e >> 11) << 10) | (((e >> 5) & 63u) * LC + 4 * (bit & 7u) + (bit >> 3));
-        u.head += n;
-        if (b.act) {
-            const int y = (int)(b.code >> 10);
-            const int x = u.S - LC + (int)(b.code & 1023u);
-            o = (y - 3) * W + x;
+    const int W = (int)u.src.W;
+    int o = 3;                                        // pixel (x, y - 3) of centre (3, 3)
+    const uint32_t nent = pk.nent;
+    if (nent != 0) {
+        const uint32_t lane = u.lane;
+        const bool has = lane < nent;
+        const uint32_t e = pk.e;
+        const uint32_t k = (uint32_t)__popc(e & 0xffffu);
+        const uint32_t inc = wave_incl_scan(k);
+        const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+        if (total >= 64u || (force && total != 0u)) {
+            b.n = min(total, 64u);
+            const uint32_t excl = inc - k;
+            uint32_t m = e & 0xffffu, pos = excl;
+            const uint32_t rl = (e >> 16) << 4;       // (row - ys) << 10 | lane << 4
+            for (;;) {
+                const bool wr = m != 0u && pos < 64u;
+                if (wave_ballot(wr) == 0) break;
+                if (wr) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    sh.stage[pos] = rl | ((bit & 3u) << 2) | (bit >> 2);
+                    ++pos;
+                }
+            }
+            // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
+            const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
+            if (has && excl < 64u && inc > 64u)
+                sh.pq[(u.head + lane) & (kSweepPixelQ - 1)] = (e & 0xffff0000u) | m;
+            u.head += nfull;
+            b.act = lane < b.n;
+            if (b.act) {
+                const uint32_t sc = sh.stage[lane];
+                b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
+                o = ((int)(b.code >> 10) - 3) * W + u.S - LC + (int)(b.code & 1023u);
+            }
         }
     }
     // the windows stay inside the frame: rows y-3 .. y+3 are rows, and the 1-2 bytes past
@@ -165,6 +221,11 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
     b.a5 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 2, 5 * W, 0));
     b.a6 = __builtin_amdgcn_raw_buffer_load_b32(u.src.rs, o - 1, 6 * W, 0);
     return b;
+}
+
+template <int LC>
+__device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, bool force) {
+    return issue_batch<LC>(sh, u, force, fifo_peek(sh, u));
 }
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
@@ -268,12 +329,9 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
             inflight[q] = false;
         }
     }
+    if (u.flags & kFlagNoFullTest) u.head = u.tail;
     while (u.tail != u.head) {
-        if (u.flags & kFlagNoFullTest) {
-            u.head = u.tail;
-            break;
-        }
-        const Batch b = issue_batch<LC>(sh, u, min(u.tail - u.head, 64u));
+        const Batch b = issue_batch<LC>(sh, u, true);
         evaluate_batch<NMS, N, LC>(sh, u, lk, b);
     }
 }
@@ -300,6 +358,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     }
     const int p0 = u.p0, p1 = u.p1;                    // rows run through the pre-filter
     const int ys = p0 - 3;                             // first row of vertical comparisons
+    u.ys = ys;
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
     u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
     u.head = u.tail = 0;
@@ -326,6 +385,8 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
         RowV cand = (RowV)(0u);                                                              \
+        FifoPeek peek;                                                                       \
+        if (((J) % kIssue) == kIssue - 1) peek = fifo_peek(sh, u);                           \
         Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);                  \
         const RowV s = Rw[((J) + 3) % K];                  /* row yv + 3 */                  \
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
@@ -356,26 +417,24 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 cand[m] = br | ~nd;                                                          \
             }                                                                                \
         }                                                                                    \
-        /* candidate pixels into the FIFO, one per lane per round: column 4m + j of the */   \
-        /* lane is bit 8j + m of cm; the entry keeps the bit, issue_batch decodes it */      \
-        const uint32_t code_base = ((uint32_t)yv << 11) | (lane << 5);                       \
+        /* the lane row's candidates into the FIFO as one entry: column 4m + j of the */     \
+        /* lane is bit 8j + m of cm, then bit 4j + m of the 16-bit mask */                   \
         uint32_t cm = 0;                                                                     \
         _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= (cand[m] >> (7 - m)) & (0x01010101u << m); \
         cm &= vmask;                                                                         \
-        for (;;) {                                                                           \
-            const bool has = cm != 0;                                                        \
+        {                                                                                    \
+            const uint32_t cx = cm | (cm >> 4);                                              \
+            const uint32_t m16 = __builtin_amdgcn_perm(cx, cx, 0x0c0c0200u);                 \
+            const bool has = m16 != 0u;                                                      \
             const uint64_t bal = wave_ballot(has);                                           \
-            if (bal == 0) break;                                                             \
-            if (has) {                                                                       \
+            if (has)                                                                         \
                 sh.pq[(u.tail + lanes_below(bal)) & (kSweepPixelQ - 1)] =                    \
-                    code_base | (uint32_t)__builtin_ctz(cm);                                 \
-                cm &= cm - 1;                                                                \
-            }                                                                                \
+                    ((uint32_t)(i0 + (J)) << 22) | (lane << 16) | m16;                       \
             u.tail += (uint32_t)__popcll(bal);                                               \
-            if (u.tail - u.head > kSweepPixelQ - 64) {                                       \
-                /* dense image: test the oldest batch now, synchronously */                  \
-                if (u.flags & kFlagNoFullTest) u.head += 64;                                 \
-                else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, 64u));     \
+            while (u.tail - u.head > kSweepPixelQ - 64) {                                    \
+                /* dense image: test the oldest pixels now, synchronously */                 \
+                if (u.flags & kFlagNoFullTest) u.head = u.tail;                              \
+                else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, true));    \
             }                                                                                \
         }                                                                                    \
         if (((J) % kIssue) == kIssue - 1) {                                                  \
@@ -385,12 +444,9 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);                             \
                 inflight[q] = false;                                                         \
             }                                                                                \
-            const uint32_t pend = u.tail - u.head;                                           \
-            const bool go = pend >= 64;                                                      \
-            if (go && (u.flags & kFlagNoFullTest)) u.head += 64u;                            \
-            const uint32_t n = (go && !(u.flags & kFlagNoFullTest)) ? 64u : 0u;              \
-            batch[q] = issue_batch<LC>(sh, u, n);                                            \
-            inflight[q] = n != 0;                                                            \
+            if (u.flags & kFlagNoFullTest) u.head = u.tail;                                  \
+            batch[q] = issue_batch<LC>(sh, u, false, peek);                                  \
+            inflight[q] = batch[q].n != 0;                                                   \
         }                                                                                    \
     }
 
@@ -809,6 +865,7 @@ void fast_sweep_kernel(BandParams P) {
 
     SweepShared sh;
     sh.pq = reinterpret_cast<uint32_t*>(smem_raw + L.pq + wave * L.wave_bytes);
+    sh.stage = reinterpret_cast<uint32_t*>(smem_raw + L.stage + wave * 64 * 4);
     sh.bitmap = bitmap;
     sh.slist = reinterpret_cast<uint32_t*>(smem_raw + L.slist);
     sh.slist_n = unit_ctr + 1;
