@@ -111,12 +111,16 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) 
     // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
     // the most owned rows per sweep step; a grid that cannot fill the chip takes the
     // shortest sweep (one 8-step block per unit) for the lowest latency.
+    // FDF_MIN_TASKS (tests): the grid size that counts as filling the chip, so that a small
+    // job can run the full-size geometry (tall bands, long units)
+    uint64_t min_tasks = 1024;
+    if (const char* m = std::getenv("FDF_MIN_TASKS")) min_tasks = std::strtoull(m, nullptr, 0);
     double best = -1.0;
     g.R = 0;
     for (uint32_t R = g.nsub; R <= 256 && R < centre_rows + g.nsub; R += g.nsub) {
         if (fdfk::make_sweep_layout(R, nw, nms).total > budget) break;
         const uint64_t tasks = (uint64_t)n_frames * ((centre_rows + R - 1) / R);
-        if (tasks < 1024) break;
+        if (tasks < min_tasks) break;
         const uint32_t steps = fdfk::sweep_steps(R / g.nsub, halo);
         const double eff = (double)R / (double)(steps * g.nsub);
         if (eff > best + 1e-9) { best = eff; g.R = R; }

@@ -152,8 +152,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // a batch the loads are still issued (all lanes at a harmless address): the pipelined issue
 // points load unconditionally, so that every path through the sweep has the same sequence
 // of loads and the compiler's vmcnt counts stay exact.
-// The FIFO entries a batch is built from: read early (the issue step's first instruction)
-// so the LDS latency hides behind the step's pre-filter work.
+// The FIFO entries a batch is built from (read when the batch is built: a read earlier in
+// the step goes stale when the step's overflow path takes entries).
 struct FifoPeek {
     uint32_t nent;         // entries read (wave-uniform)
     uint32_t e;            // this lane's entry (0 past nent)
@@ -385,8 +385,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
         RowV cand = (RowV)(0u);                                                              \
-        FifoPeek peek;                                                                       \
-        if (((J) % kIssue) == kIssue - 1) peek = fifo_peek(sh, u);                           \
         Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);                  \
         const RowV s = Rw[((J) + 3) % K];                  /* row yv + 3 */                  \
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
@@ -445,7 +443,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 inflight[q] = false;                                                         \
             }                                                                                \
             if (u.flags & kFlagNoFullTest) u.head = u.tail;                                  \
-            batch[q] = issue_batch<LC>(sh, u, false, peek);                                  \
+            batch[q] = issue_batch<LC>(sh, u, false);                                        \
             inflight[q] = batch[q].n != 0;                                                   \
         }                                                                                    \
     }

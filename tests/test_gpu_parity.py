@@ -147,6 +147,36 @@ def test_1080p(gen):
         assert_same(img, t, n, nms)
 
 
+@pytest.fixture
+def full_geometry(monkeypatch):
+    """Run small jobs with the full-size geometry (tall bands, long units, pipelined batches
+    and FIFO overflow) that large batches get: fdf_api.cpp pick_geometry reads
+    FDF_MIN_TASKS on every call."""
+    monkeypatch.setenv("FDF_MIN_TASKS", "1")
+
+
+@pytest.mark.parametrize("gen", ["s1", "s2", "s3"])
+def test_1080p_full_geometry(full_geometry, gen):
+    img = {"s1": workloads.s1_frame(5), "s2": workloads.s2_frame(1),
+           "s3": workloads.s3_frame(2)}[gen]
+    for t, n, nms in ((16, 9, 0), (16, 9, 1), (16, 9, 2), (10, 12, 1)):
+        assert_same(img, t, n, nms)
+
+
+def test_batch_full_geometry(full_geometry):
+    frames = np.stack([workloads.s1_frame(i) for i in range(3)] + [workloads.s3_frame(7)])
+    cfg = Config(16, 9, NonMaximalSuppression.MaxThreshold)
+    pts, offs = fast_hip.detector_batch(frames, cfg)
+    for f in range(frames.shape[0]):
+        assert np.array_equal(pts[offs[f]:offs[f + 1]], oracle.detect(frames[f], 16, 9, 1)), f
+
+
+def test_4k_full_geometry(full_geometry):
+    img = workloads.s1_frame(3, 3840, 2160)
+    assert_same(img, 8, 12, 2)
+    assert_same(img, 16, 9, 0)
+
+
 def test_4k_t8_n12_sad():
     """BASELINE config 5 shape: 3840x2160 t=8 n=12 SAD."""
     assert_same(workloads.s1_frame(1, 3840, 2160), 8, 12, 2)
