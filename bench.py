@@ -158,6 +158,59 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, 
     return res
 
 
+def rgb_path(fast_hip, cfg, frames, out, offs, stream, nframes=256, steps=10):
+    """SURVEY.md §8 row f4 on this GPU: device-resident RGB8 frames -> rgb_to_luma_kernel ->
+    detector.  The RGB frames repeat each grey frame's byte in all three channels, so their
+    luma is the grey frame itself and the keypoints must equal the grey path's.  The luma
+    kernel moves 4 algorithmic bytes per pixel (3 read, 1 written)."""
+    import torch
+
+    F, H, W = min(nframes, frames.shape[0]), frames.shape[1], frames.shape[2]
+    grey_in = frames[:F]
+    rgb = grey_in.unsqueeze(-1).expand(F, H, W, 3).contiguous()
+    grey = torch.empty((F, H, W), dtype=torch.uint8, device=frames.device)
+    offs_rgb = torch.zeros(F + 1, dtype=torch.int64, device=frames.device)
+    for _ in range(3):
+        fast_hip.rgb_to_luma(rgb, grey, stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        fast_hip.rgb_to_luma(rgb, grey, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    luma_ms = sorted(s.elapsed_time(e) for s, e in ev)[steps // 2]
+    for _ in range(3):
+        fast_hip.rgb_to_luma(rgb, grey, stream=stream)
+        fast_hip.detect_device(grey, cfg, out, offs_rgb, stream=stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fast_hip.rgb_to_luma(rgb, grey, stream=stream)
+        fast_hip.detect_device(grey, cfg, out, offs_rgb, stream=stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    same = bool(torch.equal(grey, grey_in))
+    n_rgb = int(offs_rgb[-1].item())
+    pts_rgb = out[:n_rgb].clone()
+    fast_hip.detect_device(grey_in, cfg, out, offs, stream=stream)
+    torch.cuda.synchronize()
+    n_grey = int(offs[F].item())
+    gbps = 4.0 * F * H * W / (luma_ms * 1e-3) / 1e9
+    res = {"workload": f"batch of {F} {W}x{H} RGB8 frames (grey repeated per channel)",
+           "Mpix_s": round(F * H * W * steps / elapsed / 1e6, 1),
+           "ms_per_step": round(elapsed * 1e3 / steps, 4),
+           "luma_kernel_ms_p50": round(luma_ms, 4),
+           "luma_kernel_GBps": round(gbps, 1),
+           "luma_roofline_frac": round(gbps / HBM_PEAK_GBS, 4),
+           "luma_equals_grey": same,
+           "keypoints_per_step": n_rgb,
+           "keypoints_equal_grey_path": n_rgb == n_grey and bool(torch.equal(pts_rgb, out[:n_grey]))}
+    del rgb, grey, pts_rgb
+    return res
+
+
 def main(argv=None):
     args = parse_args(argv)
     world, rank, local = dist_env()
@@ -271,6 +324,7 @@ def main(argv=None):
             extras[f"single_frame_{name}_kp"] = int(offs[1].item())
         extras["config5_4k"] = config5_4k(fast_hip, Config, NonMaximalSuppression, workloads,
                                           out, stream, device)
+        extras["rgb_path"] = rgb_path(fast_hip, cfg, frames, out, offs, stream)
         if world == 1 and args.cpu_seconds > 0:
             cpu, cpu_mt = cpu_baseline(args, nms)
             extras["cpu_baseline_all_cores"] = cpu_mt

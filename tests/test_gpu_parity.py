@@ -177,6 +177,25 @@ def test_4k_full_geometry(full_geometry):
     assert_same(img, 16, 9, 0)
 
 
+@pytest.mark.parametrize("nms", [0, 1, 2])
+def test_full_geometry_every_n(full_geometry, nms):
+    """Dense candidates (blurred noise, low threshold) keep the FIFO near full in every unit,
+    so the overflow path runs inside issue steps for every circle count."""
+    rng = np.random.default_rng(77)
+    img = rng.integers(0, 256, (1080, 1920), dtype=np.uint8)
+    img[::2] = img[1::2]                                   # some 2-row structure
+    for n in range(9, 17):
+        assert_same(img, 6 if n < 13 else 3, n, nms)
+
+
+@pytest.mark.parametrize("shape", [(613, 1001), (1500, 37), (9, 2000), (1079, 1919)])
+def test_full_geometry_ragged(full_geometry, shape):
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    img = (rng.integers(0, 256, shape, dtype=np.uint8) // 3 * 3).astype(np.uint8)
+    for nms in (0, 1, 2):
+        assert_same(img, 12, 9, nms)
+
+
 def test_4k_t8_n12_sad():
     """BASELINE config 5 shape: 3840x2160 t=8 n=12 SAD."""
     assert_same(workloads.s1_frame(1, 3840, 2160), 8, 12, 2)
