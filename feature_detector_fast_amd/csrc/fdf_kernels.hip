@@ -129,39 +129,55 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
             if (o[q] < P.cap) P.out[o[q]] = v[q];
     }
 
-    // bitmap bands: one wave each, 64 words per round, in raster order
-    for (uint32_t i = wave; i < ntask_here; i += kCompactTasks / 64) {
-        const uint32_t tk = first + i;
+    // bitmap bands (more points than their slot holds): the whole group expands each one,
+    // kExpandWords consecutive words per thread per round (16-byte loads, all in flight), a
+    // block scan of the threads' point counts giving every thread its output position
+    constexpr uint32_t kExpandWords = 8;
+    for (uint32_t i = 0; i < ntask_here; ++i) {          // uniform over the group
         const uint32_t n = s_task_off[i + 1 < ntask_here ? i + 1 : kCompactTasks] - s_task_off[i];
         if (n <= slot_pts) continue;
+        const uint32_t tk = first + i;
         const uint8_t* slot = P.slots + (uint64_t)tk * P.slot_bytes;
         const uint32_t frame = tk / P.bands_per_frame;
         const uint32_t band = tk - frame * P.bands_per_frame;
         const uint32_t y0 = 3 + band * P.rows;
         const uint32_t rows = min(P.rows, P.height - 3 - y0);
         const uint32_t nwords = rows * P.words_per_row;
-        const uint32_t* words = reinterpret_cast<const uint32_t*>(slot);
+        // the slot is 16-byte aligned and a multiple of 16 bytes long, so a 16-byte load
+        // starting below nwords stays inside it; words from nwords on are masked
+        const uint4* words4 = reinterpret_cast<const uint4*>(slot);
         unsigned long long o = base + s_task_off[i];
-        for (uint32_t w0 = 0; w0 < nwords; w0 += 64) {
-            const uint32_t w = w0 + lane;
-            uint32_t bits = w < nwords ? words[w] : 0u;
-            const uint32_t c = __popc(bits);
-            uint32_t inc = c;
+        for (uint32_t w0 = 0; w0 < nwords; w0 += kExpandWords * kCompactTasks) {
+            const uint32_t wt = w0 + tid * kExpandWords;   // this thread's first word
+            uint32_t bits[kExpandWords];
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t v = __shfl_up(inc, d, 64);
-                if (lane >= (uint32_t)d) inc += v;
+            for (uint32_t q = 0; q < kExpandWords / 4; ++q) {
+                const uint32_t w = wt + 4 * q;
+                const uint4 v = w < nwords ? words4[w / 4] : make_uint4(0u, 0u, 0u, 0u);
+                bits[4 * q] = v.x; bits[4 * q + 1] = v.y; bits[4 * q + 2] = v.z; bits[4 * q + 3] = v.w;
             }
-            unsigned long long k = o + inc - c;
-            const uint32_t r = w / P.words_per_row;
-            const uint32_t xb = (w - r * P.words_per_row) * 32;
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
-                if (k < P.cap) P.out[k] = make_uint2(xb + bit, y0 + r);
-                ++k;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < kExpandWords; ++q) {
+                if (wt + q >= nwords) bits[q] = 0u;
+                c += __popc(bits[q]);
             }
-            o += __shfl(inc, 63, 64);
+            uint32_t round_total;
+            unsigned long long k = o + block_exclusive_scan(c, s_wave_sum, round_total);
+#pragma unroll
+            for (uint32_t q = 0; q < kExpandWords; ++q) {
+                const uint32_t w = wt + q;
+                const uint32_t r = w / P.words_per_row;
+                const uint32_t xb = (w - r * P.words_per_row) * 32;
+                uint32_t bq = bits[q];
+                while (bq) {
+                    const uint32_t bit = __builtin_ctz(bq);
+                    bq &= bq - 1;
+                    if (k < P.cap) P.out[k] = make_uint2(xb + bit, y0 + r);
+                    ++k;
+                }
+            }
+            o += round_total;
         }
     }
 }

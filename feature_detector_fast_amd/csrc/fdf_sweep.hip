@@ -545,7 +545,10 @@ __device__ __forceinline__ uint32_t nms_collect(const uint32_t* bitmap, uint32_t
         }
     }
     __syncthreads();
-    return *list_n;
+    const uint32_t n = *list_n;
+    // every wave has its count before a second call (band_nms) resets it
+    __syncthreads();
+    return n;
 }
 
 // Pass 2 + 3 of band_nms on a complete list (LDS or global): compare, then clear.
