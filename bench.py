@@ -124,7 +124,7 @@ def cpu_baseline(args, nms):
 
 
 def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, device,
-               frames=128, steps=10):
+               oracle_detect, frames=128, steps=10):
     """BASELINE.json config 5 on this GPU: 3840x2160 S1 frames, t=8 n=12 (3-of-4 cardinal
     pre-filter), SAD NMS; 128 frames = 1.06 GB, the same bytes per launch as config 4."""
     import torch
@@ -147,13 +147,26 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, 
     ctx.set_timing(False)
     kernel_ms = sweep_ms / max(calls, 1)
     alg = frames * W * H
+    # parity outside the timed region: one more launch must repeat the last one exactly, and
+    # frame 0 and the densest frame must equal the CPU oracle
+    total = int(offs[-1].item())
+    o1 = offs.cpu().numpy().copy()
+    p1 = out[: min(total, out.shape[0])].cpu().numpy().copy()
+    fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
+    torch.cuda.synchronize()
+    repeat_ok = bool(np.array_equal(offs.cpu().numpy(), o1)) and bool(
+        np.array_equal(out[: len(p1)].cpu().numpy(), p1))
+    checked = sorted({0, int(np.argmax(np.diff(o1)))})
+    exact = all(np.array_equal(p1[o1[f]:o1[f + 1]].astype(np.uint32),
+                               oracle_detect(batch[f].cpu().numpy(), 8, 12, 2)) for f in checked)
     res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad",
            "Mpix_s": round(alg * steps / elapsed / 1e6, 1),
            "ms_per_step": round(elapsed * 1e3 / steps, 4),
            "kernel_ms_avg": round(kernel_ms, 4),
            "compaction_kernel_ms_avg": round(compact_ms / max(calls, 1), 4),
            "roofline_frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "keypoints_per_step": int(offs[-1].item())}
+           "keypoints_per_step": total,
+           "parity": {"oracle_frames": checked, "bit_exact": exact, "repeat_identical": repeat_ok}}
     del batch
     return res
 
@@ -323,7 +336,7 @@ def main(argv=None):
             extras[f"single_frame_{name}_Mpix_s"] = round(W * H / (lat[len(lat) // 2] * 1e-3) / 1e6, 1)
             extras[f"single_frame_{name}_kp"] = int(offs[1].item())
         extras["config5_4k"] = config5_4k(fast_hip, Config, NonMaximalSuppression, workloads,
-                                          out, stream, device)
+                                          out, stream, device, oracle.detect)
         extras["rgb_path"] = rgb_path(fast_hip, cfg, frames, out, offs, stream)
         if world == 1 and args.cpu_seconds > 0:
             cpu, cpu_mt = cpu_baseline(args, nms)
