@@ -1,0 +1,79 @@
+"""Batch-scale stress of the HIP path: thresholds x circle counts x NMS modes on full-size
+batches (the geometry the bench runs: tall bands, long units, FIFO overflow, LDS score-list
+overflow, bitmap slots).  Every case launches twice and compares the two results on the
+device (races show up as run-to-run differences), then checks the densest frames and frame 0
+against the CPU oracle.  Needs an MI355X."""
+import numpy as np
+import pytest
+
+import workloads
+from feature_detector_fast_amd import Config, NonMaximalSuppression, fast_hip
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+W, H = 1920, 1080
+
+
+def launch_twice_and_check(frames, t, n, nms, n_check=2):
+    import torch
+
+    F = frames.shape[0]
+    cfg = Config(t, n, NonMaximalSuppression(nms))
+    offs = torch.zeros(F + 1, dtype=torch.int64, device="cuda")
+    out = torch.empty((1, 2), dtype=torch.int32, device="cuda")
+    fast_hip.detect_device(frames, cfg, out, offs)          # sizing launch
+    torch.cuda.synchronize()
+    total = int(offs[-1])
+    out = torch.empty((max(total, 1), 2), dtype=torch.int32, device="cuda")
+    fast_hip.detect_device(frames, cfg, out, offs)
+    first_pts, first_offs = out.clone(), offs.clone()
+    fast_hip.detect_device(frames, cfg, out, offs)
+    torch.cuda.synchronize()
+    assert int(first_offs[-1]) == total, (t, n, nms)
+    assert torch.equal(offs, first_offs), (t, n, nms)
+    assert torch.equal(out, first_pts), (t, n, nms)
+    o = offs.cpu().numpy()
+    counts = np.diff(o)
+    for f in sorted({0, *np.argsort(counts)[-n_check:].tolist()}):
+        got = out[o[f]:o[f + 1]].cpu().numpy().astype(np.uint32)
+        want = oracle.detect(frames[f].cpu().numpy(), t, n, nms)
+        assert np.array_equal(got, want), (f, t, n, nms, len(got), len(want))
+    return total
+
+
+@pytest.fixture(scope="module")
+def s1_batch():
+    return workloads.s1_frames_torch(0, 512, W, H)
+
+
+@pytest.mark.parametrize("nms", [0, 1, 2])
+@pytest.mark.parametrize("n", [9, 12, 16])
+@pytest.mark.parametrize("t", [3, 8, 30])
+def test_s1_batch(s1_batch, t, n, nms):
+    launch_twice_and_check(s1_batch, t, n, nms)
+
+
+@pytest.fixture(scope="module")
+def mixed_batch():
+    """64 frames: S2, S3, noise and half-noise/half-S1, interleaved."""
+    import torch
+
+    rng = np.random.default_rng(2024)
+    frames = []
+    for i in range(16):
+        frames.append(workloads.s2_frame(100 + i))
+        frames.append(workloads.s3_frame(200 + i))
+        frames.append(rng.integers(0, 256, (H, W), dtype=np.uint8))
+        half = workloads.s1_frame(300 + i)
+        half[: H // 2] = rng.integers(0, 256, (H // 2, W), dtype=np.uint8)
+        frames.append(half)
+    return torch.from_numpy(np.stack(frames)).cuda()
+
+
+@pytest.mark.parametrize("nms", [0, 1, 2])
+@pytest.mark.parametrize("n", [9, 16])
+@pytest.mark.parametrize("t", [6, 20])
+def test_mixed_batch_full_geometry(mixed_batch, monkeypatch, t, n, nms):
+    monkeypatch.setenv("FDF_MIN_TASKS", "1")      # 64 frames with the full-size geometry
+    launch_twice_and_check(mixed_batch, t, n, nms, n_check=3)
