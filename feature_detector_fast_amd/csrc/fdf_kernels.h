@@ -64,7 +64,10 @@ __host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 
 // keypoint scores: a list of kScoreListCap (position, score) entries and per-row /
 // per-4-word-block keypoint counts that turn a bitmap position into its raster rank; the
 // scores in rank order go to the FIFO area once the sweep is done.
-constexpr uint32_t kScoreListCap = 2048;
+#ifndef FDF_SLIST_CAP
+#define FDF_SLIST_CAP 2048
+#endif
+constexpr uint32_t kScoreListCap = FDF_SLIST_CAP;
 constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix block
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
