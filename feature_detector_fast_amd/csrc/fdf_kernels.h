@@ -23,6 +23,7 @@ constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compa
 constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
 constexpr uint32_t kFlagNoNms = 16;       // NMS modes: every keypoint is kept (no band NMS pass)
 constexpr uint32_t kFlagNmsPrefixOnly = 32;  // band NMS pass: rank prefixes only (timing)
+constexpr uint32_t kFlagNoEval = 64;       // batches are issued (FIFO, staging, loads), never tested
 
 // Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).

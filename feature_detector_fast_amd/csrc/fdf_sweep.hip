@@ -248,6 +248,11 @@ __device__ __forceinline__ void pack_ring(const Batch& b, uint32_t (&w)[4], uint
 template <int NMS, int N, int LC>
 __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
                                                const LerpConsts& lk, const Batch& b) {
+    if (u.flags & kFlagNoEval) {   // ablation: consume the loads, test nothing
+        if (b.act && (b.a0 ^ b.a1.x ^ b.a2.x ^ b.a3.x ^ b.a4.x ^ b.a5.x ^ b.a6) == 0x5a5a5a5au)
+            u.flags |= kFlagNoEval;
+        return;
+    }
     const int y = (int)(b.code >> 10), cl = (int)(b.code & 1023u);
     const int x = u.S - LC + cl;
     uint32_t w[4], c;
