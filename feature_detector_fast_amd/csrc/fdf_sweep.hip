@@ -145,6 +145,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// Maximum over the wave's 64 lanes, in every lane (DPP row shifts, row broadcasts, then lane
+// 63's value read back).
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Pops the next 64 candidate pixels (fewer only when `force`: a flush) and starts their
 // loads.  The FIFO holds lane rows; the pixels of the first 64 entries are counted with a
 // wave prefix sum, every contributing entry writes its pixels to the staging array in
@@ -188,6 +200,7 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             const uint32_t excl = inc - k;
             uint32_t m = e & 0xffffu, pos = excl;
             const uint32_t rl = (e >> 16) << 4;       // (row - ys) << 10 | lane << 4
+#ifdef FDF_BALLOT_EXPAND
             for (;;) {
                 const bool wr = m != 0u && pos < 64u;
                 if (wave_ballot(wr) == 0) break;
@@ -198,6 +211,19 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
                     ++pos;
                 }
             }
+#else
+            // this lane writes min(k, 64 - excl) pixels; a wave-uniform loop over the most
+            // any lane writes (no per-iteration ballot)
+            const uint32_t cnt = excl < 64u ? min(k, 64u - excl) : 0u;
+            const uint32_t iters = __builtin_amdgcn_readfirstlane(wave_max(cnt));
+            for (uint32_t it = 0; it < iters; ++it) {
+                if (it < cnt) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    sh.stage[pos + it] = rl | ((bit & 3u) << 2) | (bit >> 2);
+                }
+            }
+#endif
             // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
             const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
             if (has && excl < 64u && inc > 64u)
