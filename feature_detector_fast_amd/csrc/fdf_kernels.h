@@ -20,7 +20,7 @@ constexpr int kCompactTasks = 256;            // tasks per workgroup of the comp
 constexpr uint32_t kFlagNoFullTest = 1;   // candidates are never tested (no keypoints)
 constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (counts only)
 constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compaction only)
-constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, never pre-filtered
+constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, no candidates
 constexpr uint32_t kFlagNoNms = 16;       // NMS modes: every keypoint is kept (no band NMS pass)
 constexpr uint32_t kFlagNmsPrefixOnly = 32;  // band NMS pass: rank prefixes only (timing)
 constexpr uint32_t kFlagNoEval = 64;       // batches are issued (FIFO, staging, loads), never tested

@@ -412,6 +412,13 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
+    // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
+    // their candidates masked: a branch around it costs the zeroing of `cand` on every step.
+#ifdef FDF_LIVE_BRANCH
+#define FDF_LIVE_TEST(l) (l)
+#else
+#define FDF_LIVE_TEST(l) true
+#endif
 #define FDF_SWEEP_STEP(J)                                                                    \
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
@@ -421,8 +428,8 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
-        const bool live = yv >= p0 && yv < p1;                                               \
-        if (live && !(u.flags & kFlagNoLoad)) {                                              \
+        const bool live = yv >= p0 && yv < p1 && !(u.flags & kFlagNoLoad);                  \
+        if (FDF_LIVE_TEST(live)) {                                                           \
             RowV e;                                                                          \
             _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
             e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
@@ -450,7 +457,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         /* lane is bit 8j + m of cm, then bit 4j + m of the 16-bit mask */                   \
         uint32_t cm = 0;                                                                     \
         _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= (cand[m] >> (7 - m)) & (0x01010101u << m); \
-        cm &= vmask;                                                                         \
+        cm &= live ? vmask : 0u;                                                             \
         {                                                                                    \
             const uint32_t cx = cm | (cm >> 4);                                              \
             const uint32_t m16 = __builtin_amdgcn_perm(cx, cx, 0x0c0c0200u);                 \
@@ -505,6 +512,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         }
     }
 #undef FDF_SWEEP_STEP
+#undef FDF_LIVE_TEST
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
