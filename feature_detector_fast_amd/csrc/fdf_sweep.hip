@@ -993,6 +993,7 @@ void fast_sweep_kernel(BandParams P) {
     const uint32_t* keep = bitmap + halo * nw;
 
     // ---- count keep-bits and write the band slot
+#ifdef FDF_EMIT_PER_THREAD
     const uint32_t per = (nwords + kThreads - 1) / kThreads;
     const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);
     uint32_t mine = 0;
@@ -1032,6 +1033,50 @@ void fast_sweep_kernel(BandParams P) {
         uint32_t* words = reinterpret_cast<uint32_t*>(slot);
         for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
     }
+#else
+    // Each wave owns a contiguous quarter of the bitmap and sweeps it 64 words per round (lane
+    // = word): the word reads are independent and conflict-free, and a wave prefix sum of the
+    // words' keypoint counts places the round's points consecutively in the slot.
+    const uint32_t wq = (nwords + kWaves - 1) / kWaves;
+    const uint32_t wb = min(wave * wq, nwords), we = min(wb + wq, nwords);
+    uint32_t mine = 0;
+    for (uint32_t w = wb + lane; w < we; w += 64) mine += __popc(keep[w]);
+    const uint32_t wave_total = __builtin_amdgcn_readlane(wave_incl_scan(mine), 63);
+    if (lane == 0) wave_sum[wave] = wave_total;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const uint32_t v = wave_sum[w];
+        before += (uint32_t)w < wave ? v : 0u;
+        total += v;
+    }
+    if (tid == 0) P.counts[task] = total;
+    if (P.flags & kFlagNoEmit) return;
+    uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
+    if (total <= P.slot_bytes / 8) {
+        uint2* pts = reinterpret_cast<uint2*>(slot);
+        uint32_t o = before;
+        for (uint32_t w0 = wb; w0 < we; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            uint32_t bits = w < we ? keep[w] : 0u;
+            const uint32_t c = __popc(bits);
+            const uint32_t inc = wave_incl_scan(c);
+            uint32_t idx = o + inc - c;
+            o += __builtin_amdgcn_readlane(inc, 63);
+            const uint32_t r = w / nw;
+            const uint32_t xb = (w - r * nw) * 32;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                pts[idx++] = make_uint2(xb + bit, y0 + r);
+            }
+        }
+    } else {
+        uint32_t* words = reinterpret_cast<uint32_t*>(slot);
+        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
+    }
+#endif
 }
 
 typedef void (*SweepKernelFn)(BandParams);
