@@ -39,7 +39,14 @@ oracle/libfast_avx2.so: oracle/fast_avx2.cpp
 tests/cpp/test_cpp_api: tests/cpp/test_cpp_api.cpp include/fdf.hpp include/fdf.h $(LIBFDF)
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG) -lfdf -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
 
+# Ablation build (tools/ablate.py, tools/pmc_ablate.sh): the same library with the internal
+# FDF_DEBUG_FLAGS / FDF_NSUB / FDF_LDS_BUDGET / FDF_COMPACT_TPG switches compiled in.
+debug: build/libfdf_debug.so
+
+build/libfdf_debug.so: $(CSRC)/*.hip $(CSRC)/*.cpp $(CSRC)/*.h include/fdf.h
+	bash tools/build_variant.sh debug "-DFDF_DEBUG_BUILD"
+
 clean:
 	rm -f $(CSRC)/*.o $(LIBFDF) oracle/*.so tests/cpp/test_cpp_api
 
-.PHONY: all clean
+.PHONY: all clean debug

@@ -33,9 +33,13 @@ NMS_NAMES = {"off": 0, "maxt": 1, "sad": 2}
 def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--frames", type=int, default=512, help="frames per GPU per step")
+    p.add_argument("--frames-total", type=int, default=0,
+                   help="strong scaling: this many frames per step in total, sharded "
+                        "contiguously over the ranks (BASELINE config 4: 512); 0 = --frames "
+                        "per GPU (weak scaling)")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--threshold", type=int, default=16)
@@ -57,6 +61,51 @@ def dist_env():
 def shard_frames(rank, frames_per_rank):
     """Frame indices owned by `rank` (weak scaling: a contiguous block per rank)."""
     return rank * frames_per_rank, frames_per_rank
+
+
+def strong_shard(rank, world, frames_total):
+    """(first, count) of `rank`'s contiguous shard of a `frames_total` batch (strong
+    scaling: shard sizes differ by at most one frame)."""
+    first = frames_total * rank // world
+    return first, frames_total * (rank + 1) // world - first
+
+
+def percentiles(v):
+    v = np.sort(np.asarray(v, dtype=np.float64))
+    if len(v) == 0:
+        return {}
+    q = lambda p: float(v[min(len(v) - 1, int(round(p * (len(v) - 1))))])
+    return {"p5": round(q(0.05), 4), "p50": round(q(0.5), 4), "p95": round(q(0.95), 4)}
+
+
+def median_ci95(v):
+    """Median and its distribution-free 95% confidence interval (order statistics)."""
+    v = np.sort(np.asarray(v, dtype=np.float64))
+    n = len(v)
+    lo = max(0, int(np.floor(n / 2 - 1.96 * np.sqrt(n) / 2)) - 1)
+    hi = min(n - 1, int(np.ceil(n / 2 + 1.96 * np.sqrt(n) / 2)))
+    return float(np.median(v)), [float(v[lo]), float(v[hi])]
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_quota():
+    """The cgroup CPU quota in cores (None when unlimited / unknown)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def reduce_max(value, world, device):
@@ -100,27 +149,92 @@ def load_traffic(cfg_key):
 
 
 def cpu_baseline(args, nms):
-    """Single-thread AVX2 port of the reference path on a bounded S1 sample (rank 0, N=1)."""
+    """The AVX2 port of the reference path (oracle/fast_avx2.cpp) on the host cores, rank 0,
+    N=1 (benches/benchmark.rs:18-50 protocol):
+      * single frame, 1 thread: NMS off / max-t / SAD, 10 warm-up calls then 100 timed calls
+        each, median and its 95% CI (config 1 is the off leg);
+      * throughput, 1 thread (the headline `cpu_baseline`): 8 S1 frames x N repetitions in
+        the bench's NMS mode, ~args.cpu_seconds of CPU work;
+      * all cores: one frame per thread over the same sample with nproc threads (and with
+        the box's CPU share), CPU model, nproc and cgroup quota stated."""
     import workloads
     from oracle import oracle
 
-    frames = np.stack([workloads.s1_frame(i, args.width, args.height) for i in range(8)])
+    W, H = args.width, args.height
+    frame = workloads.s1_frame(0, W, H)
+    single = {}
+    for name, mode in (("off", 0), ("maxt", 1), ("sad", 2)):
+        ms, kp = oracle.avx2_samples(frame, args.threshold, args.count, mode, 10, 100)
+        med, ci = median_ci95(ms)
+        single[name] = {"ms_median": round(med, 4), "ms_ci95": [round(ci[0], 4), round(ci[1], 4)],
+                        "Mpix_s": round(W * H / (med * 1e-3) / 1e6, 1), "keypoints": kp,
+                        "warmup": 10, "samples": 100}
+    frames = np.stack([workloads.s1_frame(i, W, H) for i in range(8)])
     secs1, _ = oracle.avx2_time(frames[:1], args.threshold, args.count, nms, 1, 1)
     reps = max(1, int(args.cpu_seconds / max(secs1, 1e-6) / len(frames)))
     secs, kp = oracle.avx2_time(frames, args.threshold, args.count, nms, 1, reps)
-    px = float(args.width * args.height) * len(frames) * reps
-    base = {"value": px / secs / 1e6, "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": f"{len(frames)} S1 {args.width}x{args.height} frames x {reps} reps, "
+    px = float(W * H) * len(frames) * reps
+    base = {"value": round(px / secs / 1e6, 1), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": f"{len(frames)} S1 {W}x{H} frames x {reps} reps, "
                       f"t={args.threshold} n={args.count} nms={args.nms}, 1 thread, "
                       f"AVX2 port of src/fast_simd.rs (oracle/fast_avx2.cpp), {secs:.1f} s",
-            "ms_per_frame": secs * 1e3 / (len(frames) * reps)}
-    threads = min(16, os.cpu_count() or 1)
-    reps_mt = max(1, reps * threads // 4)
-    secs_mt, _ = oracle.avx2_time(frames, args.threshold, args.count, nms, threads, reps_mt)
-    mt = {"value": px / reps * reps_mt / secs_mt / 1e6, "unit": "Mpixels/s", "cores": threads,
-          "kind": "port", "cpu": platform.processor() or platform.machine(),
-          "nproc": os.cpu_count()}
+            "ms_per_frame": round(secs * 1e3 / (len(frames) * reps), 4),
+            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "single_frame": single}
+    nproc = os.cpu_count() or 1
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = nproc
+    quota = cpu_quota()
+    legs = {}
+    for label, threads in (("nproc", nproc), ("affinity", share)):
+        if label == "affinity" and threads == nproc:
+            continue
+        # ~3 s of work spread over the threads, at least 2 frames per thread
+        reps_mt = max(1, int(3.0 * min(threads, quota or threads) / max(secs1, 1e-6) / len(frames)),
+                      2 * threads // len(frames))
+        secs_mt, _ = oracle.avx2_time(frames, args.threshold, args.count, nms, threads, reps_mt)
+        legs[label] = {"value": round(px / reps * reps_mt / secs_mt / 1e6, 1),
+                       "unit": "Mpixels/s", "threads": threads, "seconds": round(secs_mt, 2),
+                       "frames": len(frames) * reps_mt}
+    mt = {"kind": "port", "cpu": cpu_model(), "nproc": nproc, "affinity_cpus": share,
+          "cgroup_cpu_quota": quota, "nms": args.nms, **legs}
     return base, mt
+
+
+def host_latency(fast_hip, _native, frame, cfgs, samples=50):
+    """End-to-end fdf_detect on one host 1080p frame -- the literal replacement of
+    fast_simd::detector: H2D + detector + compaction + offsets/points D2H, synchronous --
+    from pageable numpy memory and from pinned (page-locked) host buffers."""
+    import ctypes
+
+    import torch
+
+    lib = _native.load()
+    ctx = fast_hip.context(0)
+    H, W = frame.shape
+    cap = W * H // 8
+    res = {}
+    pin_in = torch.from_numpy(frame).pin_memory()
+    pin_out = torch.empty((cap, 2), dtype=torch.int32).pin_memory()
+    np_out = np.empty((cap, 2), dtype=np.uint32)
+    for name, (cfg, mode) in cfgs.items():
+        c = _native.FdfConfig(cfg.threshold, cfg.count, mode)
+        for mem, (src, dst) in (("pageable", (frame.ctypes.data, np_out.ctypes.data)),
+                                ("pinned", (pin_in.data_ptr(), pin_out.data_ptr()))):
+            n = ctypes.c_size_t(0)
+            ts = []
+            for k in range(10 + samples):
+                t0 = time.perf_counter()
+                rc = lib.fdf_detect(ctx.handle, src, W, H, W, ctypes.byref(c), dst, cap,
+                                    ctypes.byref(n))
+                t1 = time.perf_counter()
+                _native.check(rc, "fdf_detect")
+                if k >= 10:
+                    ts.append((t1 - t0) * 1e3)
+            res[f"{name}_{mem}"] = {**percentiles(ts), "keypoints": n.value}
+    return res
 
 
 def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, device,
@@ -224,6 +338,75 @@ def rgb_path(fast_hip, cfg, frames, out, offs, stream, nframes=256, steps=10):
     return res
 
 
+def make_batch(workloads, first, count, W, H, device, min_bytes=0):
+    """`count` S1 frames from global index `first`, plus identical copies until the copies
+    together hold >= min_bytes: a step reads copy k % len(copies), so a shard smaller than
+    the 256 MiB Infinity Cache is still read from HBM on every step."""
+    batch = workloads.s1_frames_torch(first, count, W, H, device=device)
+    copies = [batch]
+    while min_bytes and len(copies) * batch.numel() < min_bytes:
+        copies.append(batch.clone())
+    return copies
+
+
+def timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, steps, warmup, world):
+    """W warm-up steps, then K timed steps between barriers + synchronizes; one step = one
+    fdf_detect_device launch over a batch.  Returns (wall seconds, per-launch detector ms,
+    per-launch compaction ms)."""
+    import torch
+
+    for k in range(warmup):
+        fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+    torch.cuda.synchronize()
+    # HIP events recorded by the library on the launch stream around each of its two
+    # kernels (fdf_ctx_set_timing): the detector kernel's own duration, live in the
+    # timed region
+    ctx.set_timing(True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    det, com = ctx.timing_samples()
+    ctx.set_timing(False)
+    return elapsed, det, com
+
+
+def roofline_of(det_ms, com_ms, alg_bytes, call_bytes, traffic):
+    """Roofline of the detector kernel from its per-launch HIP-event durations."""
+    sweep = float(np.mean(det_ms)) if len(det_ms) else float("nan")
+    comp = float(np.mean(com_ms)) if len(com_ms) else float("nan")
+    achieved = alg_bytes / (sweep * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "fast_sweep_kernel", "kernel_ms_avg": round(sweep, 4),
+            "kernel_ms": percentiles(det_ms), "timed_launches": int(len(det_ms)),
+            "alg_bytes_per_launch": int(alg_bytes),
+            "compaction_kernel_ms_avg": round(comp, 4), "compaction_kernel_ms": percentiles(com_ms),
+            "call_GBps": round(call_bytes / ((sweep + comp) * 1e-3) / 1e9, 1),
+            "measured_achievable_peak": 6290.0}
+
+
+def check_parity(oracle, frames, pts, offsets, first, count, t, n, nms, W):
+    """Sampled frames against the CPU oracle, raster order inside every frame."""
+    ok = True
+    checked = []
+    for f in sorted({0, count // 2, count - 1}):
+        want = oracle.detect(frames[f].cpu().numpy(), t, n, nms)
+        ok &= bool(np.array_equal(pts[offsets[f]:offsets[f + 1]], want))
+        checked.append(first + f)
+    order_ok = True
+    for f in range(count):   # raster order inside every frame (size-independent property)
+        seg = pts[offsets[f]:offsets[f + 1]].astype(np.int64)
+        if len(seg) > 1:
+            key = seg[:, 1] * W + seg[:, 0]
+            order_ok &= bool(np.all(np.diff(key) > 0))
+    return {"oracle_frames": checked, "bit_exact": ok, "raster_order": order_ok}
+
+
 def main(argv=None):
     args = parse_args(argv)
     world, rank, local = dist_env()
@@ -237,41 +420,30 @@ def main(argv=None):
     device = torch.device("cuda", local)
 
     import workloads
-    from feature_detector_fast_amd import Config, NonMaximalSuppression, fast_hip
+    from feature_detector_fast_amd import Config, NonMaximalSuppression, _native, fast_hip
     from oracle import oracle
 
     nms = NMS_NAMES[args.nms]
     cfg = Config(args.threshold, args.count, NonMaximalSuppression(nms))
-    W, H, B = args.width, args.height, args.frames
-    first, count = shard_frames(rank, B)
-    frames = workloads.s1_frames_torch(first, count, W, H, device=device)
-    cap = B * 200_000
+    W, H = args.width, args.height
+    strong = args.frames_total > 0
+    if strong:
+        first, count = strong_shard(rank, world, args.frames_total)
+    else:
+        first, count = shard_frames(rank, args.frames)
+    # a shard below 512 MiB is rotated through copies (>= 512 MiB in all), so that its frames come
+    # from HBM, not the 256 MiB Infinity Cache
+    copies = make_batch(workloads, first, count, W, H, device, min_bytes=1 << 29)
+    frames = copies[0]
+    cap = max(count, 1) * 200_000
     out = torch.empty((cap, 2), dtype=torch.int32, device=device)
-    offs = torch.zeros(B + 1, dtype=torch.int64, device=device)
+    offs = torch.zeros(count + 1, dtype=torch.int64, device=device)
     stream = torch.cuda.current_stream(device)
-
-    for _ in range(args.warmup):
-        fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
-    torch.cuda.synchronize()
-
-    # HIP events recorded by the library on the launch stream around each of its two kernels
-    # (fdf_ctx_set_timing): the detector kernel's own duration, live in the timed region
     ctx = fast_hip.context(local)
-    ctx.set_timing(True)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    elapsed = time.perf_counter() - t0
-    elapsed = reduce_max(elapsed, world, device)
-    calls, sweep_ms_total, compact_ms_total = ctx.timing()
-    ctx.set_timing(False)
-    sweep_ms_avg = sweep_ms_total / max(calls, 1)
-    compact_ms_avg = compact_ms_total / max(calls, 1)
 
+    elapsed, det, com = timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, args.steps,
+                                    args.warmup, world)
+    elapsed = reduce_max(elapsed, world, device)
     total_kp = int(offs[-1].item())
     offsets = offs.cpu().numpy()
 
@@ -279,19 +451,8 @@ def main(argv=None):
     parity = {}
     if not args.no_extras:
         pts = out[: min(total_kp, cap)].cpu().numpy().astype(np.uint32)
-        ok = True
-        checked = []
-        for f in sorted({0, count // 2, count - 1}):
-            want = oracle.detect(frames[f].cpu().numpy(), args.threshold, args.count, nms)
-            ok &= bool(np.array_equal(pts[offsets[f]:offsets[f + 1]], want))
-            checked.append(first + f)
-        order_ok = True
-        for f in range(count):   # raster order inside every frame (size-independent property)
-            seg = pts[offsets[f]:offsets[f + 1]].astype(np.int64)
-            if len(seg) > 1:
-                key = seg[:, 1] * W + seg[:, 0]
-                order_ok &= bool(np.all(np.diff(key) > 0))
-        parity = {"oracle_frames": checked, "bit_exact": ok, "raster_order": order_ok}
+        parity = check_parity(oracle, frames, pts, offsets, first, count, args.threshold,
+                              args.count, nms, W)
 
     frames_total = reduce_sum(float(count), world, device)
     kp_total = reduce_sum(float(total_kp), world, device)
@@ -303,19 +464,45 @@ def main(argv=None):
     # (DESIGN.md §5); the whole call adds the output points and frame offsets
     alg_bytes = count * W * H
     call_bytes = alg_bytes + 8 * total_kp + 8 * (count + 1)
-    achieved = alg_bytes / (sweep_ms_avg * 1e-3) / 1e9
-    cfg_key = f"{W}x{H}_b{B}_t{args.threshold}_n{args.count}_{args.nms}"
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(cfg_key), "kernel": "fast_sweep_kernel",
-                "kernel_ms_avg": round(sweep_ms_avg, 4), "timed_launches": calls,
-                "alg_bytes_per_launch": alg_bytes,
-                "compaction_kernel_ms_avg": round(compact_ms_avg, 4),
-                "call_GBps": round(call_bytes / ((sweep_ms_avg + compact_ms_avg) * 1e-3) / 1e9, 1),
-                "measured_achievable_peak": 6290.0}
+    cfg_key = f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{args.nms}"
+    roofline = roofline_of(det, com, alg_bytes, call_bytes, load_traffic(cfg_key))
 
     extras = {}
     cpu = None
+    if not args.no_extras:
+        # the other half of the headline metric ("with and without NMS"): the same batch,
+        # NMS off (or max-t when the headline is off), same protocol
+        other = "off" if nms != 0 else "maxt"
+        ocfg = Config(args.threshold, args.count, NonMaximalSuppression(NMS_NAMES[other]))
+        e2, d2, c2 = timed_steps(fast_hip, ctx, copies, ocfg, out, offs, stream, args.steps,
+                                 args.warmup, world)
+        e2 = reduce_max(e2, world, device)
+        kp2 = int(offs[-1].item())
+        pts2 = out[: min(kp2, cap)].cpu().numpy().astype(np.uint32)
+        leg = {"workload": f"same batch, nms={other}",
+               "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
+               "ms_per_step": round(e2 * 1e3 / args.steps, 4),
+               "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
+               "roofline": roofline_of(d2, c2, alg_bytes, alg_bytes + 8 * kp2 + 8 * (count + 1),
+                                       load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
+               "parity": check_parity(oracle, frames, pts2, offs.cpu().numpy(), first, count,
+                                      args.threshold, args.count, NMS_NAMES[other], W)}
+        extras[f"nms_{other}"] = leg
+        if world > 1 and not strong:
+            # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU
+            f4, c4 = strong_shard(rank, world, 512)
+            cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29)
+            off4 = torch.zeros(c4 + 1, dtype=torch.int64, device=device)
+            e4, d4, _ = timed_steps(fast_hip, ctx, cop4, cfg, out, off4, stream, args.steps,
+                                    args.warmup, world)
+            e4 = reduce_max(e4, world, device)
+            extras["config4_strong"] = {
+                "workload": f"512 {W}x{H} frames in total, {c4} per GPU (rank {rank}), "
+                            f"nms={args.nms}; rotated through {len(cop4)} copies (HBM reads)",
+                "value": round(512 * W * H / e4 * args.steps / 1e6, 1), "unit": "Mpixels/s",
+                "ms_per_step": round(e4 * 1e3 / args.steps, 4), "scaling": "strong",
+                "kernel_ms": percentiles(d4)}
+            del cop4
     if rank == 0 and not args.no_extras:
         # single-frame latency (device-resident frame, one launch, HIP events)
         one = frames[:1].contiguous()
@@ -335,24 +522,36 @@ def main(argv=None):
             extras[f"single_frame_{name}_ms_p50"] = round(lat[len(lat) // 2], 4)
             extras[f"single_frame_{name}_Mpix_s"] = round(W * H / (lat[len(lat) // 2] * 1e-3) / 1e6, 1)
             extras[f"single_frame_{name}_kp"] = int(offs[1].item())
+        host = frames[0].cpu().numpy()
+        extras["host_fdf_detect_ms"] = host_latency(
+            fast_hip, _native, host,
+            {"off": (cfg, 0), "maxt": (cfg, 1)})
         extras["config5_4k"] = config5_4k(fast_hip, Config, NonMaximalSuppression, workloads,
                                           out, stream, device, oracle.detect)
         extras["rgb_path"] = rgb_path(fast_hip, cfg, frames, out, offs, stream)
         if world == 1 and args.cpu_seconds > 0:
             cpu, cpu_mt = cpu_baseline(args, nms)
             extras["cpu_baseline_all_cores"] = cpu_mt
+            sf = cpu["single_frame"]
+            extras["gpu_vs_cpu_single_frame"] = {
+                k: {"cpu_avx2_ms_median": sf[k]["ms_median"],
+                    "gpu_fdf_detect_pinned_ms_p50": extras["host_fdf_detect_ms"].get(f"{k}_pinned", {}).get("p50"),
+                    "gpu_device_resident_ms_p50": extras.get(f"single_frame_{k}_ms_p50")}
+                for k in ("off", "maxt")}
 
     if rank == 0:
+        work = (f"{args.frames_total} {W}x{H} frames per step in total, {count} per GPU"
+                if strong else f"batch of {count} {W}x{H} frames per GPU")
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mpixels/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic S1 (committed 300x200 golden fixture tiled, rolled per frame)",
-            "config": {"workload": f"batch of {B} {W}x{H} frames per GPU, t={args.threshold} "
-                                   f"n={args.count} nms={args.nms}",
-                       "frames_per_gpu": B, "width": W, "height": H,
+            "config": {"workload": f"{work}, t={args.threshold} n={args.count} nms={args.nms}",
+                       "frames_per_gpu": count, "width": W, "height": H,
                        "threshold": args.threshold, "count": args.count, "nms": args.nms,
+                       "hbm_copies": len(copies),
                        "parallelism": f"frame-sharded x{world} (no collective)"},
             "keypoints_per_step": int(kp_total),
             "roofline": roofline,

@@ -36,7 +36,8 @@ EXPORTED_SYMBOLS = (
     "fdf_detect_batch", "fdf_detect_device", "fdf_score_points", "fdf_detect_scored",
     "fdf_detect_batch_scored", "fdf_score_device", "fdf_pipeline_create",
     "fdf_pipeline_destroy", "fdf_pipeline_acquire", "fdf_pipeline_submit", "fdf_pipeline_push",
-    "fdf_pipeline_collect",
+    "fdf_pipeline_collect", "fdf_ctx_set_geometry", "fdf_ctx_timing_samples", "fdf_fetch_last",
+    "fdf_detect_batch_multi", "fdf_fetch_last_multi",
 )
 
 
@@ -143,6 +144,17 @@ def load():
     lib.fdf_pipeline_push.argtypes = [vp, vp, u32, sz, ctypes.POINTER(u64)]
     lib.fdf_pipeline_collect.restype = ctypes.c_int
     lib.fdf_pipeline_collect.argtypes = [vp, u64, vp, vp, sz, vp, ctypes.POINTER(sz)]
+    lib.fdf_ctx_set_geometry.restype = ctypes.c_int
+    lib.fdf_ctx_set_geometry.argtypes = [vp, u32]
+    lib.fdf_ctx_timing_samples.restype = ctypes.c_int
+    lib.fdf_ctx_timing_samples.argtypes = [vp, vp, vp, u32, ctypes.POINTER(u32)]
+    lib.fdf_fetch_last.restype = ctypes.c_int
+    lib.fdf_fetch_last.argtypes = [vp, vp, vp, sz, ctypes.POINTER(sz)]
+    lib.fdf_detect_batch_multi.restype = ctypes.c_int
+    lib.fdf_detect_batch_multi.argtypes = [vp, u32, vp, u32, u32, u32, sz, cfgp, vp, sz, vp,
+                                           ctypes.POINTER(sz)]
+    lib.fdf_fetch_last_multi.restype = ctypes.c_int
+    lib.fdf_fetch_last_multi.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz)]
     del u8p
     _lib = lib
     return lib
@@ -182,6 +194,24 @@ class Context:
         check(self._lib.fdf_ctx_timing(self.handle, ctypes.byref(n), ctypes.byref(a),
                                        ctypes.byref(b)))
         return n.value, a.value, b.value
+
+    def timing_samples(self):
+        """Per-call (detector_ms, compaction_ms) arrays since timing was enabled."""
+        import numpy as np
+
+        n = ctypes.c_uint32()
+        check(self._lib.fdf_ctx_timing_samples(self.handle, None, None, 0, ctypes.byref(n)))
+        det = np.zeros(n.value, dtype=np.float32)
+        com = np.zeros(n.value, dtype=np.float32)
+        if n.value:
+            check(self._lib.fdf_ctx_timing_samples(self.handle, det.ctypes.data, com.ctypes.data,
+                                                   n.value, ctypes.byref(n)))
+        return det, com
+
+    def set_geometry(self, min_tasks=0):
+        """Band geometry override (fdf_ctx_set_geometry): min_tasks=1 gives small jobs the
+        tall bands of large batches (tests); 0 restores the default."""
+        check(self._lib.fdf_ctx_set_geometry(self.handle, int(min_tasks)))
 
     def close(self):
         if self.handle:

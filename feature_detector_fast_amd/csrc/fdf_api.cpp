@@ -10,12 +10,23 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <new>
 
 #include "../../include/fdf.h"
 #include "fdf_kernels.h"
+
+// Result of the last host-API detection on a context (fdf_fetch_last): its points stay in
+// d_out, its offsets in d_offsets and its frames in d_in until the next host call.
+struct LastResult {
+    bool valid = false;
+    uint64_t total = 0;
+    uint32_t n_frames = 0, width = 0, height = 0;
+    fdf_config cfg{};
+};
 
 struct fdf_ctx {
     int device = 0;
@@ -30,6 +41,16 @@ struct fdf_ctx {
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
     uint8_t* d_map = nullptr;           size_t map_bytes = 0;      // NMS score map
+    // cross-stream ordering: the device work of the last enqueue (on any stream) completes
+    // at `done`; the next enqueue on another stream waits for it first
+    hipEvent_t done = nullptr;
+    hipStream_t done_stream = nullptr;
+    bool done_valid = false;
+    // the last enqueue's compaction, relaunched when the host output has to grow
+    fdfk::CompactParams last_compact{};
+    LastResult last;
+    // grid size that counts as filling the chip (fdf_ctx_set_geometry; 0 = kDefaultMinTasks)
+    uint64_t min_tasks = 0;
     // optional per-kernel timing (fdf_ctx_set_timing): 3 events around each call's launches
     bool timing = false;
     size_t timed = 0;                     // calls recorded since timing was enabled
@@ -37,6 +58,7 @@ struct fdf_ctx {
 };
 
 constexpr size_t kMaxTimedCalls = 4096;
+constexpr uint64_t kDefaultMinTasks = 1024;   // 4 workgroups on each of 256 CUs
 
 namespace {
 
@@ -68,16 +90,28 @@ int check_shape(uint32_t w, uint32_t h, int* empty) {
     return FDF_OK;
 }
 
+// The device work of the last enqueue (whatever stream it ran on) has finished.
+void wait_done(fdf_ctx* ctx) {
+    if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
+}
+
+// Grow a workspace buffer to `need` elements (+1/8 headroom).  The old buffer may still be
+// read by work on another stream, so everything the context enqueued is drained first.
 template <typename T>
-int ensure(T** buf, size_t* have, size_t need, bool zero, hipStream_t stream) {
+int ensure(fdf_ctx* ctx, T** buf, size_t* have, size_t need, hipStream_t stream) {
     if (*have >= need) return FDF_OK;
-    if (*buf) { (void)hipStreamSynchronize(stream); (void)hipFree(*buf); *buf = nullptr; *have = 0; }
-    size_t n = std::max(need, *have * 2);
+    if (*buf) {
+        wait_done(ctx);
+        (void)hipStreamSynchronize(stream);
+        (void)hipFree(*buf);
+        *buf = nullptr;
+        *have = 0;
+    }
+    const size_t n = need + need / 8;
     if (hipMalloc(reinterpret_cast<void**>(buf), n * sizeof(T)) != hipSuccess) {
         *buf = nullptr;
         return FDF_ERR_ALLOC;
     }
-    if (zero && hipMemsetAsync(*buf, 0, n * sizeof(T), stream) != hipSuccess) return FDF_ERR_DEVICE;
     *have = n;
     return FDF_OK;
 }
@@ -91,14 +125,17 @@ struct Geometry {
 };
 
 
-Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) {
+Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
+                       uint64_t min_tasks) {
     Geometry g;
     const uint32_t sc = (uint32_t)fdfk::strip_cols(fdfk::kLaneCols);
     g.nstrips = (w - 3 + sc - 1) / sc;
     // >= 4 units per band (one per wave), handed out dynamically; taller units (fewer halo
     // rows) measured faster than more, shorter units for balance
     g.nsub = (4 + g.nstrips - 1) / g.nstrips;
-    if (const char* e = std::getenv("FDF_NSUB")) g.nsub = (uint32_t)std::strtoul(e, nullptr, 0);
+#ifdef FDF_DEBUG_BUILD   // ablation builds only (libfdf_debug.so)
+    if (const char* e = std::getenv("FDF_NSUB")) g.nsub = std::max(1ul, std::strtoul(e, nullptr, 0));
+#endif
     const uint32_t centre_rows = h - 6;
     const uint32_t nw = (w + 31) / 32;
     // extra rows a unit tests: NMS bands test one row above and below (first / last unit)
@@ -107,14 +144,15 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) 
     // Without NMS a 35 KB budget (bands of ~122 rows at 1080p) measured faster than the
     // tallest band that fits (more, shorter workgroups: a shorter grid tail).
     uint32_t budget = nms ? 40000u : 35000u;
-    if (const char* b = std::getenv("FDF_LDS_BUDGET")) budget = (uint32_t)std::strtoul(b, nullptr, 0);
-    // Among band heights whose grid fills the chip (>= 1024 workgroups), take the one with
-    // the most owned rows per sweep step; a grid that cannot fill the chip takes the
-    // shortest sweep (one 8-step block per unit) for the lowest latency.
-    // FDF_MIN_TASKS (tests): the grid size that counts as filling the chip, so that a small
-    // job can run the full-size geometry (tall bands, long units)
-    uint64_t min_tasks = 1024;
-    if (const char* m = std::getenv("FDF_MIN_TASKS")) min_tasks = std::strtoull(m, nullptr, 0);
+#ifdef FDF_DEBUG_BUILD
+    if (const char* b = std::getenv("FDF_LDS_BUDGET"))
+        budget = std::min<uint32_t>(fdfk::kSweepMaxLds, (uint32_t)std::strtoul(b, nullptr, 0));
+#endif
+    // Among band heights whose grid fills the chip (>= min_tasks workgroups), take the one
+    // with the most owned rows per sweep step; a grid that cannot fill the chip takes the
+    // shortest sweep (one ring block per unit) for the lowest latency.  min_tasks = 1
+    // (fdf_ctx_set_geometry, tests) gives a small job the full-size geometry (tall bands,
+    // long units); the keypoints are the same either way.
     double best = -1.0;
     g.R = 0;
     for (uint32_t R = g.nsub; R <= 256 && R < centre_rows + g.nsub; R += g.nsub) {
@@ -134,12 +172,15 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms) 
     return g;
 }
 
-// Enqueue detection + compaction over `n_frames` device frames (w, h >= 7).
+// Enqueue detection + compaction over `n_frames` device frames (w, h >= 7) on `stream`,
+// after the context's previous device work (which may have run on another stream: the
+// workspace is shared).
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream) {
     const uint32_t sb = fdfk::score_bytes_for(cfg->nms);
-    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms);
+    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms,
+                                       ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
     if (fdfk::make_sweep_layout(R, nw, cfg->nms).total > fdfk::kSweepMaxLds)
@@ -149,16 +190,27 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
     const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw);
     uint32_t tpg = fdfk::compact_tasks_per_group((uint32_t)ntasks);
-    if (const char* e = std::getenv("FDF_COMPACT_TPG"))   // ablation runs only
+    uint32_t flags = 0;
+#ifdef FDF_DEBUG_BUILD   // ablation builds only (libfdf_debug.so), see fdf_kernels.h
+    if (const char* e = std::getenv("FDF_COMPACT_TPG"))
         tpg = std::max(1u, std::min((uint32_t)fdfk::kCompactTasks, (uint32_t)std::strtoul(e, nullptr, 0)));
+    if (const char* dbg = std::getenv("FDF_DEBUG_FLAGS")) flags = (uint32_t)std::strtoul(dbg, nullptr, 0);
+#endif
+    if (!ctx->done &&
+        hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming) != hipSuccess) {
+        ctx->done = nullptr;
+        return FDF_ERR_DEVICE;
+    }
+    if (ctx->done_valid && ctx->done_stream != stream &&
+        hipStreamWaitEvent(stream, ctx->done, 0) != hipSuccess)
+        return FDF_ERR_DEVICE;
     int rc;
-    if ((rc = ensure(&ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), false, stream))) return rc;
-    if ((rc = ensure(&ctx->d_counts, &ctx->counts_n, (size_t)ntasks, false, stream))) return rc;
+    if ((rc = ensure(ctx, &ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), stream))) return rc;
+    if ((rc = ensure(ctx, &ctx->d_counts, &ctx->counts_n, (size_t)ntasks, stream))) return rc;
     // NMS score map: written at keypoints only and read only where the keypoint bitmap
     // marks one, so it is never cleared
-    if (sb && (rc = ensure(&ctx->d_map, &ctx->map_bytes, (size_t)n_frames * w * h * sb, false, stream)))
+    if (sb && (rc = ensure(ctx, &ctx->d_map, &ctx->map_bytes, (size_t)n_frames * w * h * sb, stream)))
         return rc;
-    const char* dbg = std::getenv("FDF_DEBUG_FLAGS");   // ablation runs only, see fdf_kernels.h
     fdfk::BandParams p;
     p.frames = d_frames;
     p.frame_stride = frame_stride;
@@ -172,7 +224,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.slot_bytes = slot_bytes;
     p.slots = ctx->d_slots;
     p.counts = ctx->d_counts;
-    p.flags = dbg ? (uint32_t)std::strtoul(dbg, nullptr, 0) : 0u;
+    p.flags = flags;
     p.nstrips = geo.nstrips;
     p.nsub = geo.nsub;
     p.scores = ctx->d_map;
@@ -207,12 +259,13 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         if (hipEventRecord(ev[2], stream) != hipSuccess) return FDF_ERR_DEVICE;
         ++ctx->timed;
     }
+    ctx->last_compact = c;
+    if (hipEventRecord(ctx->done, stream) != hipSuccess) return FDF_ERR_DEVICE;
+    ctx->done_stream = stream;
+    ctx->done_valid = true;
     return FDF_OK;
 }
 
-// Shared body of fdf_detect / fdf_detect_batch: host frames in, host points out.
-// `rgb`: the frames are RGB8 (rows of 3 * w bytes at row_stride), converted on the device
-// with image 0.24.6's to_luma8 before detection (src/main.rs:58).
 // The score reported with a keypoint: the NMS mode's own, max-threshold when NMS is off.
 uint32_t score_kind(uint32_t nms) {
     return nms == FDF_NMS_SUM_ABSOLUTE ? FDF_NMS_SUM_ABSOLUTE : FDF_NMS_MAX_THRESHOLD;
@@ -223,38 +276,47 @@ uint32_t score_blocks(uint64_t points, uint32_t n_frames) {
     return (uint32_t)std::min<uint64_t>(64, per_frame / 1024 + 1);
 }
 
-int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
-                size_t row_stride, size_t frame_stride, const fdf_config* cfg, fdf_point* out,
-                size_t cap, uint64_t* frame_offsets, size_t* n_out, bool rgb = false,
-                uint16_t* out_scores = nullptr, bool scored = false) {
-    if (!ctx || !n_out || (cap && !out) || (scored && cap && !out_scores)) return FDF_ERR_ARG;
+// Validation shared by the host entry points; *empty = the reference returns no points.
+int check_host_args(const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
+                    size_t row_stride, const fdf_config* cfg, bool rgb, int* empty) {
     int rc = check_config(cfg);
     if (rc) return rc;
-    int empty = 0;
-    rc = check_shape(w, h, &empty);
+    rc = check_shape(w, h, empty);
     if (rc) return rc;
-    if (n_frames == 0) empty = 1;
-    if (!data && !empty) return FDF_ERR_ARG;
+    if (n_frames == 0) *empty = 1;
+    if (!data && !*empty) return FDF_ERR_ARG;
     if (row_stride < (rgb ? 3ull * w : (size_t)w)) return FDF_ERR_ARG;
-    if (empty) {
-        *n_out = 0;
-        if (frame_offsets) std::memset(frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull));
-        return FDF_OK;
-    }
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    DeviceGuard guard(ctx->device);
+    return FDF_OK;
+}
+
+// Phase 1 of a host detection (lock held): frames in, detection + compaction into the
+// context's output buffer, frame offsets back to the host (`offs`, n_frames + 1 entries).
+// The device output starts small and grows to the keypoint total; when it has to grow only
+// the compaction is run again (the per-band slots still hold the detection).  On success
+// ctx->last describes the result, which stays on the device until the next host call.
+// `rgb`: the frames are RGB8 (rows of 3 * w bytes at row_stride), converted on the device
+// with image 0.24.6's to_luma8 before detection (src/main.rs:58).
+int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
+             size_t row_stride, size_t frame_stride, const fdf_config* cfg, bool rgb,
+             uint64_t* offs) {
+    ctx->last.valid = false;
     const size_t frame_bytes = (size_t)w * h;
     const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
-    if ((rc = ensure(&ctx->d_in, &ctx->in_bytes, frame_bytes * n_frames, false, ctx->stream))) return rc;
-    if ((rc = ensure(&ctx->d_out, &ctx->out_points, max_points, false, ctx->stream))) return rc;
-    if ((rc = ensure(&ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, false, ctx->stream))) return rc;
+    // first guess: 1 keypoint per 64 pixels (real images: 0.5-1.5 per 100)
+    const size_t guess = std::min(max_points, std::max<size_t>(4096, frame_bytes / 64 * n_frames));
+    int rc;
+    if ((rc = ensure(ctx, &ctx->d_in, &ctx->in_bytes, frame_bytes * n_frames, ctx->stream))) return rc;
+    if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, guess, ctx->stream))) return rc;
+    if ((rc = ensure(ctx, &ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, ctx->stream))) return rc;
     const size_t px = rgb ? 3 : 1;                 // bytes per pixel of the host frames
     uint8_t* stage = ctx->d_in;
     if (rgb) {
-        if ((rc = ensure(&ctx->d_rgb, &ctx->rgb_bytes, 3 * frame_bytes * n_frames, false, ctx->stream)))
+        if ((rc = ensure(ctx, &ctx->d_rgb, &ctx->rgb_bytes, 3 * frame_bytes * n_frames, ctx->stream)))
             return rc;
         stage = ctx->d_rgb;
     }
+    // the host frames are read by the copies below: nothing else may still read d_in
+    wait_done(ctx);
     for (uint32_t f = 0; f < n_frames; ++f) {
         const uint8_t* src = data + (size_t)f * frame_stride;
         uint8_t* dst = stage + (size_t)f * frame_bytes * px;
@@ -268,38 +330,102 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
     if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
-    rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, ctx->d_out, max_points,
+    rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, ctx->d_out, ctx->out_points,
                  ctx->d_offsets, ctx->stream);
     if (rc) return rc;
-    uint64_t* offs = frame_offsets;
-    uint64_t local[2];
-    if (!offs) offs = n_frames == 1 ? local : new (std::nothrow) uint64_t[n_frames + 1ull];
-    if (!offs) return FDF_ERR_ALLOC;
     hipError_t e = hipMemcpyAsync(offs, ctx->d_offsets, sizeof(uint64_t) * (n_frames + 1ull),
                                   hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    const uint64_t total = offs[n_frames];
-    if (offs != frame_offsets && offs != local) delete[] offs;
     if (e != hipSuccess) return FDF_ERR_DEVICE;
-    const size_t ncopy = (size_t)std::min<uint64_t>(total, cap);
-    if (scored && ncopy) {
-        if ((rc = ensure(&ctx->d_scores, &ctx->scores_n, ncopy, false, ctx->stream))) return rc;
-        e = fdfk::launch_score_frames(ctx->d_in, w, frame_bytes, n_frames, ctx->d_out,
-                                      ctx->d_offsets, ncopy, score_blocks(ncopy, n_frames),
-                                      score_kind(cfg->nms), cfg->threshold, cfg->count,
-                                      ctx->d_scores, ctx->stream);
+    const uint64_t total = offs[n_frames];
+    if (total > ctx->out_points) {
+        // grow the output and compact again (the offsets do not change)
+        fdfk::CompactParams c = ctx->last_compact;
+        if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (size_t)total, ctx->stream))) return rc;
+        c.out = ctx->d_out;
+        c.cap = ctx->out_points;
+        if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
+            hipEventRecord(ctx->done, ctx->stream) != hipSuccess)
+            return FDF_ERR_DEVICE;
+        ctx->done_stream = ctx->stream;
+    }
+    ctx->last.valid = true;
+    ctx->last.total = total;
+    ctx->last.n_frames = n_frames;
+    ctx->last.width = w;
+    ctx->last.height = h;
+    ctx->last.cfg = *cfg;
+    return FDF_OK;
+}
+
+// Phase 2 (lock held): copy the first `n` points of the last result, and their scores when
+// `out_scores` is given, to the host.
+int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
+    if (!n) return FDF_OK;
+    const LastResult& L = ctx->last;
+    hipError_t e = hipSuccess;
+    if (out_scores) {
+        int rc = ensure(ctx, &ctx->d_scores, &ctx->scores_n, n, ctx->stream);
+        if (rc) return rc;
+        e = fdfk::launch_score_frames(ctx->d_in, L.width, (uint64_t)L.width * L.height,
+                                      L.n_frames, ctx->d_out, ctx->d_offsets, n,
+                                      score_blocks(n, L.n_frames), score_kind(L.cfg.nms),
+                                      L.cfg.threshold, L.cfg.count, ctx->d_scores, ctx->stream);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(out_scores, ctx->d_scores, ncopy * sizeof(uint16_t),
+            e = hipMemcpyAsync(out_scores, ctx->d_scores, n * sizeof(uint16_t),
                                hipMemcpyDeviceToHost, ctx->stream);
-        if (e != hipSuccess) return FDF_ERR_DEVICE;
     }
-    if (ncopy) {
-        e = hipMemcpyAsync(out, ctx->d_out, ncopy * sizeof(fdf_point), hipMemcpyDeviceToHost,
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(out, ctx->d_out, n * sizeof(fdf_point), hipMemcpyDeviceToHost,
                            ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e != hipSuccess) return FDF_ERR_DEVICE;
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
+}
+
+// Shared body of fdf_detect / fdf_detect_batch / the scored and RGB variants: host frames
+// in, host points out.  With `cap` below the total, the first `cap` points are written,
+// FDF_ERR_CAPACITY is returned and the whole result stays on the device for fdf_fetch_last.
+int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
+                size_t row_stride, size_t frame_stride, const fdf_config* cfg, fdf_point* out,
+                size_t cap, uint64_t* frame_offsets, size_t* n_out, bool rgb = false,
+                uint16_t* out_scores = nullptr, bool scored = false) {
+    if (!ctx || !n_out || (cap && !out) || (scored && cap && !out_scores)) return FDF_ERR_ARG;
+    int empty = 0;
+    int rc = check_host_args(data, n_frames, w, h, row_stride, cfg, rgb, &empty);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (empty) {
+        ctx->last = LastResult{};
+        ctx->last.valid = true;
+        ctx->last.cfg = *cfg;
+        *n_out = 0;
+        if (frame_offsets) std::memset(frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull));
+        return FDF_OK;
     }
+    DeviceGuard guard(ctx->device);
+    std::vector<uint64_t> local;
+    uint64_t* offs = frame_offsets;
+    if (!offs) {
+        local.resize(n_frames + 1ull);
+        offs = local.data();
+    }
+    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs);
+    if (rc) return rc;
+    const uint64_t total = offs[n_frames];
+    rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
+    if (rc) return rc;
     *n_out = (size_t)total;
+    return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
+}
+
+// Copy of the last host result (fdf_fetch_last), lock held.
+int fetch_last(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t cap, size_t* n_out) {
+    if (!ctx->last.valid) return FDF_ERR_ARG;
+    DeviceGuard guard(ctx->device);
+    const uint64_t total = ctx->last.total;
+    *n_out = (size_t)total;
+    const int rc = copy_out(ctx, out, out_scores, (size_t)std::min<uint64_t>(total, cap));
+    if (rc) return rc;
     return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
 
@@ -359,6 +485,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
     if (!ctx) return;
     {
         DeviceGuard guard(ctx->device);
+        wait_done(ctx);
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(ctx->d_in);
         (void)hipFree(ctx->d_rgb);
@@ -369,6 +496,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_map);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
+        if (ctx->done) (void)hipEventDestroy(ctx->done);
         (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -381,6 +509,29 @@ int fdf_ctx_set_timing(fdf_ctx* ctx, int enable) {
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->timing = enable != 0;
     ctx->timed = 0;
+    return FDF_OK;
+}
+
+int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
+    if (!ctx) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->min_tasks = min_tasks;
+    return FDF_OK;
+}
+
+int fdf_ctx_timing_samples(fdf_ctx* ctx, float* detect_ms, float* compact_ms, uint32_t cap,
+                           uint32_t* n) {
+    if (!ctx || !n || (cap && (!detect_ms || !compact_ms))) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    *n = (uint32_t)ctx->timed;
+    for (size_t k = 0; k < ctx->timed && k < cap; ++k) {
+        const hipEvent_t* e = &ctx->ev[3 * k];
+        if (hipEventSynchronize(e[2]) != hipSuccess ||
+            hipEventElapsedTime(&detect_ms[k], e[0], e[1]) != hipSuccess ||
+            hipEventElapsedTime(&compact_ms[k], e[1], e[2]) != hipSuccess)
+            return FDF_ERR_DEVICE;
+    }
     return FDF_OK;
 }
 
@@ -408,6 +559,13 @@ int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t heigh
                size_t* n_out) {
     return detect_host(ctx, data, 1, width, height, stride_bytes, 0, cfg, out, cap, nullptr,
                        n_out);
+}
+
+int fdf_fetch_last(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t cap,
+                   size_t* n_out) {
+    if (!ctx || !n_out || (cap && !out)) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    return fetch_last(ctx, out, out_scores, cap, n_out);
 }
 
 int fdf_detect_rgb(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
@@ -526,9 +684,11 @@ int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t
     std::lock_guard<std::mutex> lock(ctx->mu);
     DeviceGuard guard(ctx->device);
     const size_t frame_bytes = (size_t)width * height;
+    ctx->last.valid = false;              // d_in / d_out are reused below
+    wait_done(ctx);
     int rc;
-    if ((rc = ensure(&ctx->d_in, &ctx->in_bytes, frame_bytes, false, ctx->stream))) return rc;
-    if ((rc = ensure(&ctx->d_out, &ctx->out_points, n_points + (n_points + 3) / 4, false,
+    if ((rc = ensure(ctx, &ctx->d_in, &ctx->in_bytes, frame_bytes, ctx->stream))) return rc;
+    if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, n_points + (n_points + 3) / 4,
                      ctx->stream)))
         return rc;
     hipError_t e = stride_bytes == width
@@ -547,6 +707,112 @@ int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t
                            ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
+}
+
+// ---- multi-device batch: contiguous frame shards, one host thread per context ----------
+
+int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* data,
+                           uint32_t n_frames, uint32_t width, uint32_t height,
+                           size_t frame_stride_bytes, const fdf_config* cfg, fdf_point* out,
+                           size_t cap, uint64_t* frame_offsets, size_t* n_out) {
+    if (!ctxs || n_ctx == 0 || n_ctx > 1024 || !n_out || (cap && !out)) return FDF_ERR_ARG;
+    for (uint32_t k = 0; k < n_ctx; ++k) {
+        if (!ctxs[k]) return FDF_ERR_ARG;
+        for (uint32_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return FDF_ERR_ARG;   // each shard needs its own workspace
+    }
+    if (n_frames > 1 && frame_stride_bytes < (size_t)width * height) return FDF_ERR_ARG;
+    int empty = 0;
+    int rc = check_host_args(data, n_frames, width, height, width, cfg, false, &empty);
+    if (rc) return rc;
+    std::vector<uint64_t> offs(n_frames + 1ull, 0);
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (uint32_t k = 0; k < n_ctx; ++k) locks.emplace_back(ctxs[k]->mu);   // held throughout
+    if (empty) {
+        for (uint32_t k = 0; k < n_ctx; ++k) {
+            ctxs[k]->last = LastResult{};
+            ctxs[k]->last.valid = true;
+            ctxs[k]->last.cfg = *cfg;
+        }
+        *n_out = 0;
+        if (frame_offsets) std::memset(frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull));
+        return FDF_OK;
+    }
+    // shard k: frames [first[k], first[k+1]) (contiguous, sizes differ by at most one)
+    std::vector<uint32_t> first(n_ctx + 1);
+    for (uint32_t k = 0; k <= n_ctx; ++k) first[k] = (uint32_t)((uint64_t)n_frames * k / n_ctx);
+    std::vector<std::vector<uint64_t>> local(n_ctx);
+    std::vector<int> status(n_ctx, FDF_OK);
+    auto detect_shard = [&](uint32_t k) {
+        fdf_ctx* ctx = ctxs[k];
+        const uint32_t nf = first[k + 1] - first[k];
+        ctx->last = LastResult{};
+        if (nf == 0) {
+            ctx->last.valid = true;
+            ctx->last.cfg = *cfg;
+            return;
+        }
+        DeviceGuard guard(ctx->device);
+        local[k].assign(nf + 1ull, 0);
+        status[k] = run_host(ctx, data + (size_t)first[k] * frame_stride_bytes, nf, width, height,
+                             width, frame_stride_bytes, cfg, false, local[k].data());
+    };
+    auto run_all = [&](auto&& fn) {
+        std::vector<std::thread> pool;
+        for (uint32_t k = 1; k < n_ctx; ++k) pool.emplace_back(fn, k);
+        fn(0u);
+        for (auto& t : pool) t.join();
+    };
+    run_all(detect_shard);
+    for (uint32_t k = 0; k < n_ctx; ++k)
+        if (status[k]) return status[k];
+    // global offsets: shard k's points follow shards 0 .. k-1
+    std::vector<uint64_t> base(n_ctx + 1, 0);
+    for (uint32_t k = 0; k < n_ctx; ++k) {
+        const uint32_t nf = first[k + 1] - first[k];
+        for (uint32_t f = 0; f < nf; ++f) offs[first[k] + f] = base[k] + local[k][f];
+        base[k + 1] = base[k] + (nf ? local[k][nf] : 0);
+    }
+    const uint64_t total = base[n_ctx];
+    offs[n_frames] = total;
+    if (frame_offsets) std::memcpy(frame_offsets, offs.data(), sizeof(uint64_t) * (n_frames + 1ull));
+    auto copy_shard = [&](uint32_t k) {
+        const uint64_t b = std::min<uint64_t>(base[k], cap), e = std::min<uint64_t>(base[k + 1], cap);
+        if (e <= b) return;
+        DeviceGuard guard(ctxs[k]->device);
+        status[k] = copy_out(ctxs[k], out + b, nullptr, (size_t)(e - b));
+    };
+    run_all(copy_shard);
+    for (uint32_t k = 0; k < n_ctx; ++k)
+        if (status[k]) return status[k];
+    *n_out = (size_t)total;
+    return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
+}
+
+int fdf_fetch_last_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, fdf_point* out, size_t cap,
+                         size_t* n_out) {
+    if (!ctxs || n_ctx == 0 || n_ctx > 1024 || !n_out || (cap && !out)) return FDF_ERR_ARG;
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (uint32_t k = 0; k < n_ctx; ++k) {
+        if (!ctxs[k]) return FDF_ERR_ARG;
+        for (uint32_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return FDF_ERR_ARG;
+        locks.emplace_back(ctxs[k]->mu);
+        if (!ctxs[k]->last.valid) return FDF_ERR_ARG;
+    }
+    uint64_t b = 0;
+    for (uint32_t k = 0; k < n_ctx; ++k) {
+        const uint64_t n = ctxs[k]->last.total;
+        const uint64_t lo = std::min<uint64_t>(b, cap), hi = std::min<uint64_t>(b + n, cap);
+        if (hi > lo) {
+            DeviceGuard guard(ctxs[k]->device);
+            const int rc = copy_out(ctxs[k], out + lo, nullptr, (size_t)(hi - lo));
+            if (rc) return rc;
+        }
+        b += n;
+    }
+    *n_out = (size_t)b;
+    return b > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
 
 }  // extern "C"

@@ -16,7 +16,9 @@ constexpr uint32_t kMaxLds = 64 * 1024;       // default dynamic-LDS limit per w
 constexpr int kCompactTasks = 256;            // tasks per workgroup of the compaction kernel
 
 // Internal ablation switches (BandParams::flags), set from the FDF_DEBUG_FLAGS environment
-// variable by the host layer; never part of the C ABI.  Results are wrong when set.
+// variable by the host layer of the debug build only (make debug -> libfdf_debug.so, built
+// with -DFDF_DEBUG_BUILD); never part of the C ABI.  Results are wrong when set.  In the
+// production build the kernels see the constant 0 and the ablation branches compile away.
 constexpr uint32_t kFlagNoFullTest = 1;   // candidates are never tested (no keypoints)
 constexpr uint32_t kFlagNoEmit = 2;       // bands write no slot contents (counts only)
 constexpr uint32_t kFlagNoPrefilter = 4;  // no units are swept (slots and compaction only)
@@ -24,6 +26,11 @@ constexpr uint32_t kFlagNoLoad = 8;       // rows are streamed and compared, no 
 constexpr uint32_t kFlagNoNms = 16;       // NMS modes: every keypoint is kept (no band NMS pass)
 constexpr uint32_t kFlagNmsPrefixOnly = 32;  // band NMS pass: rank prefixes only (timing)
 constexpr uint32_t kFlagNoEval = 64;       // batches are issued (FIFO, staging, loads), never tested
+#ifdef FDF_DEBUG_BUILD
+__host__ __device__ inline uint32_t ablation_flags(uint32_t f) { return f; }
+#else
+__host__ __device__ inline uint32_t ablation_flags(uint32_t) { return 0u; }
+#endif
 
 // Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).
@@ -69,6 +76,8 @@ __host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 
 #define FDF_SLIST_CAP 2048
 #endif
 constexpr uint32_t kScoreListCap = FDF_SLIST_CAP;
+// band_nms_lds ranks the list's scores as u16 into the 4 candidate FIFOs
+static_assert(kScoreListCap * 2 <= 4 * kSweepPixelQ * 4, "ranked scores must fit the FIFO area");
 constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix block
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;

@@ -221,6 +221,10 @@ int fdf_pipeline_submit(fdf_pipeline* p, uint64_t ticket, uint32_t n_frames) {
     s->n_frames = n_frames;
     s->state = kSubmitted;
     s->error = enqueue_batch(p, *s, n_frames);   // reported by collect
+    // a batch that failed part-way may still have its frame copy in flight: drain the slot's
+    // stream, so that its staging buffer is free once collect releases the slot (the
+    // batch's done event was not recorded for this ticket)
+    if (s->error) (void)hipStreamSynchronize(s->stream);
     return FDF_OK;
 }
 
@@ -253,7 +257,7 @@ int fdf_pipeline_collect(fdf_pipeline* p, uint64_t ticket, fdf_point* out,
         done = s->done;
     }
     DeviceGuard guard(p->device);
-    const hipError_t we = hipEventSynchronize(done);
+    const hipError_t we = s->error ? hipSuccess : hipEventSynchronize(done);
     std::lock_guard<std::mutex> lock(p->mu);
     s->state = kSubmitted;
     if (s->error || we != hipSuccess) {   // a failed batch is dropped with its error

@@ -274,7 +274,7 @@ __device__ __forceinline__ void pack_ring(const Batch& b, uint32_t (&w)[4], uint
 template <int NMS, int N, int LC>
 __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
                                                const LerpConsts& lk, const Batch& b) {
-    if (u.flags & kFlagNoEval) {   // ablation: consume the loads, test nothing
+    if (ablation_flags(u.flags) & kFlagNoEval) {   // ablation: consume the loads, test nothing
         if (b.act && (b.a0 ^ b.a1.x ^ b.a2.x ^ b.a3.x ^ b.a4.x ^ b.a5.x ^ b.a6) == 0x5a5a5a5au)
             u.flags |= kFlagNoEval;
         return;
@@ -360,7 +360,7 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
             inflight[q] = false;
         }
     }
-    if (u.flags & kFlagNoFullTest) u.head = u.tail;
+    if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;
     while (u.tail != u.head) {
         const Batch b = issue_batch<LC>(sh, u, true);
         evaluate_batch<NMS, N, LC>(sh, u, lk, b);
@@ -428,7 +428,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
-        const bool live = yv >= p0 && yv < p1 && !(u.flags & kFlagNoLoad);                  \
+        const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
         if (FDF_LIVE_TEST(live)) {                                                           \
             RowV e;                                                                          \
             _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
@@ -469,7 +469,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             u.tail += (uint32_t)__popcll(bal);                                               \
             while (u.tail - u.head > kSweepPixelQ - 64) {                                    \
                 /* dense image: test the oldest pixels now, synchronously */                 \
-                if (u.flags & kFlagNoFullTest) u.head = u.tail;                              \
+                if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                              \
                 else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, true));    \
             }                                                                                \
         }                                                                                    \
@@ -480,7 +480,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);                             \
                 inflight[q] = false;                                                         \
             }                                                                                \
-            if (u.flags & kFlagNoFullTest) u.head = u.tail;                                  \
+            if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                                  \
             batch[q] = issue_batch<LC>(sh, u, false);                                        \
             inflight[q] = batch[q].n != 0;                                                   \
         }                                                                                    \
@@ -927,14 +927,14 @@ void fast_sweep_kernel(BandParams P) {
     u.nw = nw;
     u.yb = (int)(y0 - halo);
     u.lane = lane;
-    u.flags = P.flags;
+    u.flags = ablation_flags(P.flags);
     const LerpConsts lk = lerp_consts(P.threshold);
 
     const uint32_t nunits = P.nstrips * P.nsub;
     const uint32_t sub_rows = (rows + P.nsub - 1) / P.nsub;
     // units are handed out dynamically: a wave that finishes early takes the next one
     // instead of idling at the workgroup barrier
-    if (!(P.flags & kFlagNoPrefilter)) {
+    if (!(ablation_flags(P.flags) & kFlagNoPrefilter)) {
         for (;;) {
             uint32_t unit = 0;
             if (lane == 0) unit = atomicAdd(unit_ctr, 1u);
@@ -968,12 +968,12 @@ void fast_sweep_kernel(BandParams P) {
     const uint32_t nwords = rows * nw;
     if constexpr (NMS != kNmsOff) {
         const uint32_t n = *sh.slist_n;
-        if (P.flags & kFlagNoNms) {
+        if (ablation_flags(P.flags) & kFlagNoNms) {
         } else if (n <= sh.slist_cap) {
             band_nms_lds<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, n,
                               reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                               reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), P.flags);
+                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), ablation_flags(P.flags));
         } else {
             // more keypoints than the list holds: the listed scores join the score map
             for (uint32_t i = tid; i < sh.slist_cap; i += kThreads) {
@@ -1014,7 +1014,7 @@ void fast_sweep_kernel(BandParams P) {
         total += v;
     }
     if (tid == 0) P.counts[task] = total;
-    if (P.flags & kFlagNoEmit) return;
+    if (ablation_flags(P.flags) & kFlagNoEmit) return;
     uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
     if (total <= P.slot_bytes / 8) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
@@ -1052,7 +1052,7 @@ void fast_sweep_kernel(BandParams P) {
         total += v;
     }
     if (tid == 0) P.counts[task] = total;
-    if (P.flags & kFlagNoEmit) return;
+    if (ablation_flags(P.flags) & kFlagNoEmit) return;
     uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
     if (total <= P.slot_bytes / 8) {
         uint2* pts = reinterpret_cast<uint2*>(slot);

@@ -35,6 +35,7 @@ def calculate_offsets(width):
 
 _ctx_lock = threading.Lock()
 _contexts = {}
+_shard_contexts = {}
 
 
 def context(device=0):
@@ -43,8 +44,26 @@ def context(device=0):
         ctx = _contexts.get(device)
         if ctx is None:
             ctx = _native.Context(device)
+            ctx.lock = threading.Lock()     # holds a two-call pattern together
             _contexts[device] = ctx
         return ctx
+
+
+def shard_contexts(devices):
+    """One distinct context per entry of ``devices`` (a device listed twice gets two
+    contexts), for :func:`detector_batch` over several devices."""
+    out, seen = [], {}
+    with _ctx_lock:
+        for dev in devices:
+            k = seen.get(dev, 0)
+            seen[dev] = k + 1
+            ctx = _shard_contexts.get((dev, k))
+            if ctx is None:
+                ctx = _native.Context(dev)
+                ctx.lock = threading.Lock()
+                _shard_contexts[(dev, k)] = ctx
+            out.append(ctx)
+    return out
 
 
 def _to_c_config(config):
@@ -73,6 +92,35 @@ def _as_pixels(img):
     return arr
 
 
+def capacity_guess(pixels):
+    """First output capacity of the two-call pattern: 1 keypoint per 64 pixels (real images
+    have 0.5-1.5 per 100; denser results are fetched with fdf_fetch_last, not recomputed)."""
+    return max(4096, int(pixels) // 64)
+
+
+def _two_call(ctx, pixels, call, where, scored=False):
+    """Run ``call(out_ptr, scores_ptr, cap, n_ref)`` with a guessed capacity; on
+    FDF_ERR_CAPACITY copy the retained device result out with fdf_fetch_last (the detection
+    runs once either way)."""
+    lib = _native.load()
+    cap = capacity_guess(pixels)
+    out = np.empty((cap, 2), dtype=np.uint32)
+    scores = np.empty(cap, dtype=np.uint16) if scored else None
+    n = ctypes.c_size_t(0)
+    with ctx.lock:
+        rc = call(out.ctypes.data, scores.ctypes.data if scored else None, cap, n)
+        if rc == _native.FDF_ERR_CAPACITY:
+            out = np.empty((n.value, 2), dtype=np.uint32)
+            scores = np.empty(n.value, dtype=np.uint16) if scored else None
+            rc = lib.fdf_fetch_last(ctx.handle, out.ctypes.data,
+                                    scores.ctypes.data if scored else None, n.value,
+                                    ctypes.byref(n))
+            where = "fdf_fetch_last"
+    check(rc, where)
+    k = n.value
+    return (out[:k], scores[:k]) if scored else out[:k]
+
+
 def detect_array(img, config, device=0):
     """Keypoints as a (K, 2) uint32 array of (x, y) rows in raster order."""
     arr = _as_pixels(img)
@@ -80,18 +128,10 @@ def detect_array(img, config, device=0):
     h, w = arr.shape
     ctx = context(device)
     lib = _native.load()
-    n = ctypes.c_size_t(0)
     stride = arr.strides[0] if arr.size else w
     ptr = arr.ctypes.data if arr.size else None
-    rc = lib.fdf_detect(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), None, 0, ctypes.byref(n))
-    if rc == _native.FDF_ERR_CAPACITY:
-        out = np.empty((n.value, 2), dtype=np.uint32)
-        rc = lib.fdf_detect(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), out.ctypes.data,
-                            out.shape[0], ctypes.byref(n))
-        check(rc, "fdf_detect")
-        return out[: n.value]
-    check(rc, "fdf_detect")
-    return np.empty((0, 2), dtype=np.uint32)
+    return _two_call(ctx, w * h, lambda o, _s, cap, n: lib.fdf_detect(
+        ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), o, cap, ctypes.byref(n)), "fdf_detect")
 
 
 def detector(img, config):
@@ -111,19 +151,11 @@ def detect_rgb_array(rgb, config, device=0):
     h, w = arr.shape[:2]
     ctx = context(device)
     lib = _native.load()
-    n = ctypes.c_size_t(0)
     stride = arr.strides[0] if arr.size else 3 * w
     ptr = arr.ctypes.data if arr.size else None
-    rc = lib.fdf_detect_rgb(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), None, 0,
-                            ctypes.byref(n))
-    if rc == _native.FDF_ERR_CAPACITY:
-        out = np.empty((n.value, 2), dtype=np.uint32)
-        rc = lib.fdf_detect_rgb(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg),
-                                out.ctypes.data, out.shape[0], ctypes.byref(n))
-        check(rc, "fdf_detect_rgb")
-        return out[: n.value]
-    check(rc, "fdf_detect_rgb")
-    return np.empty((0, 2), dtype=np.uint32)
+    return _two_call(ctx, w * h, lambda o, _s, cap, n: lib.fdf_detect_rgb(
+        ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), o, cap, ctypes.byref(n)),
+        "fdf_detect_rgb")
 
 
 def detector_rgb(rgb, config):
@@ -154,28 +186,48 @@ def rgb_to_luma(frames, out, stream=None, device=None):
           "fdf_rgb_to_luma_device")
 
 
-def detector_batch(frames, config, device=0):
+def detector_batch(frames, config, device=0, devices=None):
     """Detect on a (F, H, W) uint8 stack.  Returns (points (K, 2) uint32, offsets (F+1,))
-    where frame f's keypoints are points[offsets[f]:offsets[f+1]]."""
+    where frame f's keypoints are points[offsets[f]:offsets[f+1]].
+
+    ``devices``: a list of HIP device ids to shard the frames over (contiguous shards, one
+    host thread and context per entry, results in frame order: fdf_detect_batch_multi).  A
+    device may be listed more than once (several contexts on one GPU)."""
     frames = np.ascontiguousarray(np.asarray(frames), dtype=np.uint8)
     if frames.ndim != 3:
         raise ValueError("expected a (F, H, W) uint8 stack")
     f, h, w = frames.shape
     cfg = _to_c_config(config)
-    ctx = context(device)
     lib = _native.load()
     offsets = np.zeros(f + 1, dtype=np.uint64)
-    n = ctypes.c_size_t(0)
     ptr = frames.ctypes.data if frames.size else None
-    rc = lib.fdf_detect_batch(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg), None, 0,
-                              offsets.ctypes.data, ctypes.byref(n))
-    out = np.empty((0, 2), dtype=np.uint32)
-    if rc == _native.FDF_ERR_CAPACITY:
-        out = np.empty((n.value, 2), dtype=np.uint32)
-        rc = lib.fdf_detect_batch(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg),
-                                  out.ctypes.data, out.shape[0], offsets.ctypes.data,
-                                  ctypes.byref(n))
-    check(rc, "fdf_detect_batch")
+    if devices is None:
+        ctx = context(device)
+        pts = _two_call(ctx, f * h * w, lambda o, _s, cap, n: lib.fdf_detect_batch(
+            ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg), o, cap, offsets.ctypes.data,
+            ctypes.byref(n)), "fdf_detect_batch")
+        return pts, offsets
+    ctxs = shard_contexts(list(devices))
+    handles = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    cap = capacity_guess(f * h * w)
+    out = np.empty((cap, 2), dtype=np.uint32)
+    n = ctypes.c_size_t(0)
+    for c in ctxs:
+        c.lock.acquire()
+    try:
+        rc = lib.fdf_detect_batch_multi(handles, len(ctxs), ptr, f, w, h, h * w,
+                                        ctypes.byref(cfg), out.ctypes.data, cap,
+                                        offsets.ctypes.data, ctypes.byref(n))
+        where = "fdf_detect_batch_multi"
+        if rc == _native.FDF_ERR_CAPACITY:
+            out = np.empty((n.value, 2), dtype=np.uint32)
+            rc = lib.fdf_fetch_last_multi(handles, len(ctxs), out.ctypes.data, n.value,
+                                          ctypes.byref(n))
+            where = "fdf_fetch_last_multi"
+    finally:
+        for c in ctxs:
+            c.lock.release()
+    check(rc, where)
     return out[: n.value], offsets
 
 
@@ -233,21 +285,11 @@ def detect_scored_array(img, config, device=0):
     h, w = arr.shape
     ctx = context(device)
     lib = _native.load()
-    n = ctypes.c_size_t(0)
     stride = arr.strides[0] if arr.size else w
     ptr = arr.ctypes.data if arr.size else None
-    rc = lib.fdf_detect_scored(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), None, None, 0,
-                               ctypes.byref(n))
-    if rc == _native.FDF_ERR_CAPACITY:
-        out = np.empty((n.value, 2), dtype=np.uint32)
-        scores = np.empty(n.value, dtype=np.uint16)
-        rc = lib.fdf_detect_scored(ctx.handle, ptr, w, h, stride, ctypes.byref(cfg),
-                                   out.ctypes.data, scores.ctypes.data, out.shape[0],
-                                   ctypes.byref(n))
-        check(rc, "fdf_detect_scored")
-        return out[: n.value], scores[: n.value]
-    check(rc, "fdf_detect_scored")
-    return np.empty((0, 2), dtype=np.uint32), np.empty(0, dtype=np.uint16)
+    return _two_call(ctx, w * h, lambda o, sc, cap, n: lib.fdf_detect_scored(
+        ctx.handle, ptr, w, h, stride, ctypes.byref(cfg), o, sc, cap, ctypes.byref(n)),
+        "fdf_detect_scored", scored=True)
 
 
 def detector_scored(img, config):
@@ -266,20 +308,11 @@ def detector_batch_scored(frames, config, device=0):
     ctx = context(device)
     lib = _native.load()
     offsets = np.zeros(f + 1, dtype=np.uint64)
-    n = ctypes.c_size_t(0)
     ptr = frames.ctypes.data if frames.size else None
-    rc = lib.fdf_detect_batch_scored(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg), None,
-                                     None, 0, offsets.ctypes.data, ctypes.byref(n))
-    out = np.empty((0, 2), dtype=np.uint32)
-    scores = np.empty(0, dtype=np.uint16)
-    if rc == _native.FDF_ERR_CAPACITY:
-        out = np.empty((n.value, 2), dtype=np.uint32)
-        scores = np.empty(n.value, dtype=np.uint16)
-        rc = lib.fdf_detect_batch_scored(ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg),
-                                         out.ctypes.data, scores.ctypes.data, out.shape[0],
-                                         offsets.ctypes.data, ctypes.byref(n))
-    check(rc, "fdf_detect_batch_scored")
-    return out[: n.value], scores[: n.value], offsets
+    pts, scores = _two_call(ctx, f * h * w, lambda o, sc, cap, n: lib.fdf_detect_batch_scored(
+        ctx.handle, ptr, f, w, h, h * w, ctypes.byref(cfg), o, sc, cap, offsets.ctypes.data,
+        ctypes.byref(n)), "fdf_detect_batch_scored", scored=True)
+    return pts, scores, offsets
 
 
 def score_device(frames, config, points, offsets, scores, stream=None, device=None):
@@ -311,6 +344,7 @@ def score_device(frames, config, points, offsets, scores, stream=None, device=No
 
 
 __all__ = ["NORTH", "EAST", "SOUTH", "WEST", "circle", "calculate_offsets", "context",
+           "shard_contexts", "capacity_guess",
            "detect_array", "detector", "detector_batch", "detect_device", "keypoint_scores",
            "detect_scored_array", "detector_scored", "detector_batch_scored", "score_device",
            "detect_rgb_array", "detector_rgb", "rgb_to_luma",

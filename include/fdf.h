@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FDF_ABI_VERSION 1
+#define FDF_ABI_VERSION 2
 
 /* Status codes.  Shapes the reference maps to an empty Vec return FDF_OK with 0 points. */
 enum fdf_status {
@@ -93,16 +93,39 @@ void* fdf_ctx_stream(fdf_ctx* ctx);
  * number and the summed durations of both launches in ms.  Enabling resets the record. */
 int fdf_ctx_set_timing(fdf_ctx* ctx, int enable);
 int fdf_ctx_timing(fdf_ctx* ctx, uint32_t* calls, float* detect_ms, float* compact_ms);
+/* The same record per call: *n = calls recorded; the first `cap` calls' detector and
+ * compaction durations (ms) go to detect_ms[k] / compact_ms[k] (for percentiles). */
+int fdf_ctx_timing_samples(fdf_ctx* ctx, float* detect_ms, float* compact_ms, uint32_t cap,
+                           uint32_t* n);
+
+/* Geometry (extension; results never depend on it): the band height is chosen so that a
+ * launch has at least `min_tasks` workgroups when it can (default 0 = 1024, enough for 4
+ * per CU).  min_tasks = 1 makes a small job use the tall bands and long sweep units of
+ * large batches -- the parity tests reach those code paths with small inputs this way. */
+int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
 
 /*
  * Replaces fast_simd::detector(img, config) -> Vec<Point> (src/fast_simd.rs:847).
  * Host image (row-major u8, `stride_bytes` >= width; GrayImage always has stride == width),
  * host output.  Synchronous.  Two-call pattern: if `cap` is too small, returns
- * FDF_ERR_CAPACITY with *n_out = the required count and writes the first `cap` points.
+ * FDF_ERR_CAPACITY with *n_out = the required count and writes the first `cap` points; the
+ * whole result stays on the device, and fdf_fetch_last copies it out without detecting
+ * again.
  */
 int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,
                size_t stride_bytes, const fdf_config* cfg, fdf_point* out, size_t cap,
                size_t* n_out);
+
+/*
+ * Second half of the two-call pattern: the points (frames concatenated, raster order) of
+ * the last host-API detection on this context (fdf_detect, fdf_detect_rgb, fdf_detect_batch
+ * and the scored variants), and their scores when `out_scores` is not NULL (the score kind
+ * of that call's config, as fdf_detect_scored).  Only copies: no detection runs.
+ * FDF_ERR_CAPACITY again if `cap` < *n_out; FDF_ERR_ARG if the context holds no result
+ * (no host detection yet, or fdf_score_points ran since).
+ */
+int fdf_fetch_last(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t cap,
+                   size_t* n_out);
 
 /*
  * RGB variant of fdf_detect: `data` holds RGB8 pixels (rows of 3 * width bytes at
@@ -136,6 +159,22 @@ int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint3
                      fdf_point* out, size_t cap, uint64_t* frame_offsets, size_t* n_out);
 
 /*
+ * Multi-device batched variant (frames shard across GPUs with no collective).
+ * The batch is cut into n_ctx contiguous shards of (nearly) equal frame counts, shard k is
+ * detected on ctxs[k] by its own host thread (contexts may be on different devices, or
+ * several on one), and the lists are concatenated in frame order -- the same result as
+ * fdf_detect_batch on one context.  The contexts must be distinct.  Capacity semantics as
+ * fdf_detect_batch; each context keeps its shard for fdf_fetch_last_multi.
+ */
+int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* data,
+                           uint32_t n_frames, uint32_t width, uint32_t height,
+                           size_t frame_stride_bytes, const fdf_config* cfg, fdf_point* out,
+                           size_t cap, uint64_t* frame_offsets, size_t* n_out);
+/* fdf_fetch_last over the contexts of the last fdf_detect_batch_multi, concatenated. */
+int fdf_fetch_last_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, fdf_point* out, size_t cap,
+                         size_t* n_out);
+
+/*
  * Device-resident batched variant (the throughput path; nothing crosses PCIe).
  * `d_frames`, `d_out` and `d_frame_offsets` are device pointers on the context's device.
  * Asynchronous: enqueued on `stream` (a hipStream_t; NULL = the HIP null stream; pass
@@ -143,8 +182,8 @@ int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint3
  * completion d_frame_offsets[0..n_frames] holds the exclusive prefix of per-frame counts
  * and d_frame_offsets[n_frames] the total, even when the total exceeds `cap` (points with
  * index >= cap are not written).  Argument and shape errors are returned synchronously.
- * The context's workspace is reused by each call: calls on one context must be issued on
- * one stream (or otherwise serialised).  Frames before the last may be read up to 15 bytes
+ * The context's workspace is reused by each call: a call on another stream than the
+ * context's previous call first waits (on the device) for that call's work.  Frames before the last may be read up to 15 bytes
  * past their end (inside the batch allocation); the last frame is read exactly.
  */
 int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,

@@ -114,16 +114,25 @@ struct Config {
 };
 
 namespace fast_hip {
+// First capacity of the two-call pattern: 1 keypoint per 64 pixels (real images have
+// 0.5-1.5 per 100).  A denser result is copied out of the context by fdf_fetch_last, so the
+// detection runs once either way.
+inline size_t capacity_guess(const GrayView& img) {
+    const size_t px = (size_t)img.width * img.height;
+    return px / 64 > 4096 ? px / 64 : 4096;
+}
+
 // Drop-in for fast_simd::detector: result in raster order, bit-identical to the reference.
 inline std::vector<Point> detector(const GrayView& img, const Config& config, Context& ctx) {
     const fdf_config c = config.to_c();
-    std::vector<Point> out;
+    std::vector<Point> out(capacity_guess(img));
     size_t n = 0;
-    int rc = fdf_detect(ctx.get(), img.data, img.width, img.height, img.stride, &c, nullptr, 0, &n);
-    while (rc == FDF_ERR_CAPACITY) {   // two-call pattern
-        out.resize(n);
-        rc = fdf_detect(ctx.get(), img.data, img.width, img.height, img.stride, &c,
+    int rc = fdf_detect(ctx.get(), img.data, img.width, img.height, img.stride, &c,
                         reinterpret_cast<fdf_point*>(out.data()), out.size(), &n);
+    if (rc == FDF_ERR_CAPACITY) {   // two-call pattern: copy the retained result
+        out.resize(n);
+        rc = fdf_fetch_last(ctx.get(), reinterpret_cast<fdf_point*>(out.data()), nullptr,
+                            out.size(), &n);
     }
     check(rc, "fdf_detect");
     out.resize(n);

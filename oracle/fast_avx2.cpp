@@ -293,4 +293,23 @@ double fdf_avx2_time(const uint8_t* frames, uint32_t n_frames, size_t frame_stri
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// Criterion-like single-frame protocol (benches/benchmark.rs:18-50): `warmup` untimed
+// calls, then `samples` calls timed one by one (steady_clock, ms into out_ms).  The frame
+// must be padded as above.  Returns the keypoint count of one call.
+int64_t fdf_avx2_samples(const uint8_t* frame, uint32_t w, uint32_t h, uint8_t t, uint8_t n,
+                         uint8_t nms, int warmup, int samples, double* out_ms) {
+    int64_t count = 0;
+    for (int i = -warmup; i < samples; ++i) {
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<Pt> r;   // the reference allocates its Vec per call
+        if (nms == kOff) detect<kOff>(frame, w, h, t, n, r);
+        else if (nms == kMaxT) detect<kMaxT>(frame, w, h, t, n, r);
+        else detect<kSad>(frame, w, h, t, n, r);
+        const auto t1 = std::chrono::steady_clock::now();
+        count = (int64_t)r.size();
+        if (i >= 0) out_ms[i] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    }
+    return count;
+}
+
 }  // extern "C"

@@ -181,3 +181,18 @@ void fdf_oracle_rgb_to_luma(const uint8_t* rgb, uint32_t w, uint32_t h, size_t r
         }
     }
 }
+
+/* Scores of given image points with the functions above (test helper for the GPU's
+ * fdf_score_points at scale): kind 1 = max-threshold (window n, src/opencv_compat.rs:172-209),
+ * kind 2 = SAD (threshold t, :278-299).  Points must be centres (3 from every border). */
+void fdf_oracle_score_points(const uint8_t* img, size_t stride, const uint32_t* xy,
+                             size_t n_pts, uint8_t kind, uint8_t t, uint8_t n, uint16_t* out) {
+    uint8_t c16[16];
+    for (size_t k = 0; k < n_pts; ++k) {
+        const uint32_t x = xy[2 * k], y = xy[2 * k + 1];
+        const uint8_t c = img[(size_t)y * stride + x];
+        circle_values(img, stride, x, y, c16);
+        out[k] = kind == 2 ? fdf_oracle_score_sum_abs(c, c16, t)
+                           : fdf_oracle_score_max_threshold(c, c16, n);
+    }
+}

@@ -32,6 +32,10 @@ int64_t fdf_oracle_detect(const uint8_t* img, uint32_t w, uint32_t h, size_t str
                           uint8_t t, uint8_t n, uint8_t nms, uint32_t* out_xy, size_t cap,
                           uint16_t* out_scores);
 
+/* Scores of image points (test helper): kind 1 = max-threshold (window n), 2 = SAD (t). */
+void fdf_oracle_score_points(const uint8_t* img, size_t stride, const uint32_t* xy,
+                             size_t n_pts, uint8_t kind, uint8_t t, uint8_t n, uint16_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,9 @@ def _load():
         lib.fdf_oracle_detect.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_size_t, u8, u8, u8, ctypes.c_void_p,
                                           ctypes.c_size_t, ctypes.c_void_p]
+        lib.fdf_oracle_score_points.restype = None
+        lib.fdf_oracle_score_points.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                ctypes.c_size_t, u8, u8, u8, ctypes.c_void_p]
         _lib = lib
     return _lib
 
@@ -68,6 +71,9 @@ def _load_avx2():
         lib.fdf_avx2_time.argtypes = [ctypes.c_void_p, u32, ctypes.c_size_t, u32, u32, u8, u8,
                                       u8, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_uint64)]
+        lib.fdf_avx2_samples.restype = ctypes.c_int64
+        lib.fdf_avx2_samples.argtypes = [ctypes.c_void_p, u32, u32, u8, u8, u8, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_void_p]
         _avx = lib
     return _avx
 
@@ -87,6 +93,18 @@ def score_max_threshold(center, circle, n):
 
 def score_sum_abs(center, circle, t):
     return int(_load().fdf_oracle_score_sum_abs(center, _circle_buf(circle), t))
+
+
+def score_points(img, points, kind, t, n):
+    """Oracle scores (uint16) of centres `points` ((K, 2) x, y): kind 1 max-threshold with
+    window n, kind 2 SAD with threshold t."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    pts = np.ascontiguousarray(np.asarray(points, dtype=np.uint32).reshape(-1, 2))
+    out = np.zeros(pts.shape[0], dtype=np.uint16)
+    if pts.shape[0]:
+        _load().fdf_oracle_score_points(img.ctypes.data, img.shape[1], pts.ctypes.data,
+                                        pts.shape[0], int(kind), int(t), int(n), out.ctypes.data)
+    return out
 
 
 def rgb_to_luma(rgb):
@@ -161,3 +179,15 @@ def avx2_time(frames, t, n, nms, threads=1, reps=1):
     secs = _load_avx2().fdf_avx2_time(buf.ctypes.data, f, h * w, w, h, t, n, int(nms), threads,
                                       reps, ctypes.byref(total))
     return secs, int(total.value)
+
+
+def avx2_samples(img, t, n, nms, warmup=10, samples=100):
+    """Per-call wall times (ms, float64 array) of the AVX2 port on one frame after `warmup`
+    untimed calls (the reference's criterion protocol), and the keypoint count."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    buf = _padded(img)
+    out = np.zeros(samples, dtype=np.float64)
+    cnt = _load_avx2().fdf_avx2_samples(buf.ctypes.data, w, h, t, n, int(nms), warmup, samples,
+                                        out.ctypes.data)
+    return out, int(cnt)

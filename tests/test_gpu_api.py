@@ -1,0 +1,177 @@
+"""Host-API behaviour of the C ABI on the GPU: the two-call capacity pattern runs the
+detection once (fdf_fetch_last), device work on different streams is ordered, the output
+buffer grows by compacting again, the geometry override, per-launch timing samples, and the
+multi-device batch (fdf_detect_batch_multi) -- every result checked against the oracle."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import workloads
+from feature_detector_fast_amd import Config, NonMaximalSuppression, _native, fast_hip
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def test_capacity_retry_runs_one_detection():
+    """A result larger than the first capacity guess (S3: ~28% keypoints) is copied out of
+    the context with fdf_fetch_last: one detector launch per call (fdf_ctx_set_timing)."""
+    img = workloads.s3_frame(4)[:400, :600].copy()
+    cfg = Config(16, 9, NonMaximalSuppression.Off)
+    assert len(oracle.detect(img, 16, 9, 0)) > fast_hip.capacity_guess(img.size)
+    ctx = fast_hip.context(0)
+    ctx.set_timing(True)
+    try:
+        got = fast_hip.detect_array(img, cfg)
+        calls, _, _ = ctx.timing()
+    finally:
+        ctx.set_timing(False)
+    assert calls == 1
+    assert np.array_equal(got, oracle.detect(img, 16, 9, 0))
+
+
+def test_fetch_last_c_abi():
+    """fdf_detect with cap 0 -> FDF_ERR_CAPACITY + n; fdf_fetch_last with a short buffer ->
+    the first cap points and FDF_ERR_CAPACITY again; then the whole list and its scores."""
+    img = workloads.s1_frame(1, 640, 480)
+    want, want_sc = oracle.detect(img, 16, 9, 1, with_scores=True)
+    lib = _native.load()
+    ctx = fast_hip.context(0)
+    cfg = _native.FdfConfig(16, 9, 1)
+    n = ctypes.c_size_t(0)
+    with ctx.lock:
+        ctx.set_timing(True)
+        rc = lib.fdf_detect(ctx.handle, img.ctypes.data, 640, 480, 640, ctypes.byref(cfg), None,
+                            0, ctypes.byref(n))
+        assert rc == _native.FDF_ERR_CAPACITY and n.value == len(want)
+        part = np.zeros((10, 2), dtype=np.uint32)
+        rc = lib.fdf_fetch_last(ctx.handle, part.ctypes.data, None, 10, ctypes.byref(n))
+        assert rc == _native.FDF_ERR_CAPACITY and n.value == len(want)
+        assert np.array_equal(part, want[:10])
+        out = np.zeros((n.value, 2), dtype=np.uint32)
+        sc = np.zeros(n.value, dtype=np.uint16)
+        rc = lib.fdf_fetch_last(ctx.handle, out.ctypes.data, sc.ctypes.data, n.value,
+                                ctypes.byref(n))
+        calls, _, _ = ctx.timing()
+        ctx.set_timing(False)
+    assert rc == _native.FDF_OK and calls == 1
+    assert np.array_equal(out, want) and np.array_equal(sc, want_sc)
+
+
+def test_fetch_last_needs_a_result():
+    lib = _native.load()
+    c = _native.Context(0)
+    n = ctypes.c_size_t(0)
+    assert lib.fdf_fetch_last(c.handle, None, None, 0, ctypes.byref(n)) == _native.FDF_ERR_ARG
+    c.close()
+
+
+def test_output_grows_by_compacting_again():
+    """A batch whose total exceeds the context's output buffer: the buffer grows and only the
+    compaction runs again (one detector launch), the result equals the oracle."""
+    frames = np.stack([workloads.s3_frame(10 + i)[:300, :400] for i in range(6)])
+    c = _native.Context(0)
+    c.lock = __import__("threading").Lock()
+    lib = _native.load()
+    cfg = _native.FdfConfig(12, 9, 0)
+    offs = np.zeros(7, dtype=np.uint64)
+    n = ctypes.c_size_t(0)
+    c.set_timing(True)
+    out = np.zeros((6 * 300 * 400, 2), dtype=np.uint32)
+    rc = lib.fdf_detect_batch(c.handle, frames.ctypes.data, 6, 400, 300, 400 * 300,
+                              ctypes.byref(cfg), out.ctypes.data, out.shape[0],
+                              offs.ctypes.data, ctypes.byref(n))
+    calls, _, _ = c.timing()
+    c.close()
+    assert rc == _native.FDF_OK and calls == 1
+    assert n.value > fast_hip.capacity_guess(frames.size)
+    for f in range(6):
+        assert np.array_equal(out[offs[f]:offs[f + 1]], oracle.detect(frames[f], 12, 9, 0)), f
+
+
+def test_device_then_host_call_without_sync():
+    """fdf_detect_device on torch's stream, then a host call on the context's own stream,
+    with no synchronisation between them: the host call waits on the device for the first
+    call's use of the shared workspace, and both results are exact."""
+    import torch
+
+    frames = workloads.s1_frames_torch(0, 64)
+    cfg = Config(16, 9, NonMaximalSuppression.MaxThreshold)
+    out = torch.empty((64 * 20000, 2), dtype=torch.int32, device="cuda")
+    offs = torch.zeros(65, dtype=torch.int64, device="cuda")
+    img = workloads.s3_frame(3)[:500, :700].copy()
+    fast_hip.detect_device(frames, cfg, out, offs)
+    got = fast_hip.detect_array(img, cfg)           # no torch.cuda.synchronize() before
+    torch.cuda.synchronize()
+    assert np.array_equal(got, oracle.detect(img, 16, 9, 1))
+    o = offs.cpu().numpy()
+    for f in (0, 31, 63):
+        want = oracle.detect(frames[f].cpu().numpy(), 16, 9, 1)
+        assert np.array_equal(out[o[f]:o[f + 1]].cpu().numpy().astype(np.uint32), want), f
+
+
+def test_geometry_override_same_result():
+    img = workloads.s1_frame(6, 800, 600)
+    cfg = Config(16, 9, NonMaximalSuppression.SumAbsolute)
+    base = fast_hip.detect_array(img, cfg)
+    ctx = fast_hip.context(0)
+    ctx.set_geometry(1)
+    try:
+        tall = fast_hip.detect_array(img, cfg)
+    finally:
+        ctx.set_geometry(0)
+    assert np.array_equal(base, tall)
+    assert np.array_equal(base, oracle.detect(img, 16, 9, 2))
+
+
+def test_timing_samples():
+    import torch
+
+    frames = workloads.s1_frames_torch(0, 8)
+    out = torch.empty((8 * 20000, 2), dtype=torch.int32, device="cuda")
+    offs = torch.zeros(9, dtype=torch.int64, device="cuda")
+    ctx = fast_hip.context(0)
+    ctx.set_timing(True)
+    for _ in range(5):
+        fast_hip.detect_device(frames, Config(16, 9, NonMaximalSuppression.Off), out, offs)
+    det, com = ctx.timing_samples()
+    calls, d_tot, c_tot = ctx.timing()
+    ctx.set_timing(False)
+    assert calls == 5 and det.shape == (5,) and np.all(det > 0) and np.all(com > 0)
+    assert abs(float(det.sum()) - d_tot) < 1e-3 * max(d_tot, 1.0)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_device_batch(devices):
+    """Frames sharded over several contexts (all on device 0 on a 1-GPU box) give the
+    single-context result, frame for frame, and equal the oracle."""
+    frames = np.stack([workloads.s1_frame(i, 960, 540) for i in range(7)] +
+                      [workloads.s3_frame(40)[:540, :960]])
+    cfg = Config(16, 9, NonMaximalSuppression.MaxThreshold)
+    pts1, offs1 = fast_hip.detector_batch(frames, cfg)
+    ptsm, offsm = fast_hip.detector_batch(frames, cfg, devices=devices)
+    assert np.array_equal(offs1, offsm)
+    assert np.array_equal(pts1, ptsm)
+    for f in range(frames.shape[0]):
+        assert np.array_equal(ptsm[offsm[f]:offsm[f + 1]], oracle.detect(frames[f], 16, 9, 1)), f
+
+
+def test_multi_device_more_contexts_than_frames():
+    frames = np.stack([workloads.s1_frame(i, 320, 240) for i in range(2)])
+    cfg = Config(16, 9, NonMaximalSuppression.Off)
+    pts, offs = fast_hip.detector_batch(frames, cfg, devices=[0, 0, 0, 0])
+    for f in range(2):
+        assert np.array_equal(pts[offs[f]:offs[f + 1]], oracle.detect(frames[f], 16, 9, 0))
+
+
+def test_multi_device_rejects_repeated_context():
+    lib = _native.load()
+    ctx = fast_hip.context(0)
+    handles = (ctypes.c_void_p * 2)(ctx.handle.value, ctx.handle.value)
+    frames = np.zeros((2, 20, 20), dtype=np.uint8)
+    n = ctypes.c_size_t(0)
+    cfg = _native.FdfConfig(16, 9, 0)
+    rc = lib.fdf_detect_batch_multi(handles, 2, frames.ctypes.data, 2, 20, 20, 400,
+                                    ctypes.byref(cfg), None, 0, None, ctypes.byref(n))
+    assert rc == _native.FDF_ERR_ARG

@@ -148,11 +148,14 @@ def test_1080p(gen):
 
 
 @pytest.fixture
-def full_geometry(monkeypatch):
+def full_geometry():
     """Run small jobs with the full-size geometry (tall bands, long units, pipelined batches
-    and FIFO overflow) that large batches get: fdf_api.cpp pick_geometry reads
-    FDF_MIN_TASKS on every call."""
-    monkeypatch.setenv("FDF_MIN_TASKS", "1")
+    and FIFO overflow) that large batches get: fdf_ctx_set_geometry(ctx, 1) on the shared
+    device-0 context, restored afterwards."""
+    ctx = fast_hip.context(0)
+    ctx.set_geometry(1)
+    yield
+    ctx.set_geometry(0)
 
 
 @pytest.mark.parametrize("gen", ["s1", "s2", "s3"])

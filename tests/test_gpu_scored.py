@@ -81,3 +81,47 @@ def test_score_device_after_detect_device():
         assert int(offs[-1]) == len(wp)
         assert np.array_equal(out[:k].cpu().numpy().astype(np.uint32), wp[:k])
         assert np.array_equal(scores[:k].cpu().numpy().view(np.uint16), ws[:k])
+
+
+def _ring_grid(cells_x, cells_y, seed):
+    """An image of 7x7 cells, one centre each at (7i+3, 7j+3): every centre's ring and
+    centre byte lie inside its own cell.  Half the cells are uniform bytes; the other half
+    are centre +- small offsets (rings near the threshold, long arcs)."""
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, 256, (7 * cells_y, 7 * cells_x), dtype=np.uint8)
+    near = rng.integers(0, 2, (cells_y, cells_x), dtype=bool)
+    cells = img.reshape(cells_y, 7, cells_x, 7).transpose(0, 2, 1, 3)
+    centre = cells[:, :, 3, 3].astype(np.int32)
+    noise = rng.integers(-40, 41, (cells_y, cells_x, 7, 7))
+    mixed = np.clip(centre[:, :, None, None] + noise, 0, 255).astype(np.uint8)
+    cells[near] = mixed[near]
+    cells[:, :, 3, 3] = centre
+    img = cells.transpose(0, 2, 1, 3).reshape(7 * cells_y, 7 * cells_x).copy()
+    ys, xs = np.mgrid[0:cells_y, 0:cells_x]
+    pts = np.stack([7 * xs.ravel() + 3, 7 * ys.ravel() + 3], axis=1).astype(np.uint32)
+    return img, pts
+
+
+def test_score_points_at_scale():
+    """>= 1M random (ring, centre, t, n) cases through fdf_score_points against the oracle,
+    both scores, every n = 9..16 (max-t) and every t = 0..255 (SAD); the reference runs 10M
+    SAD and 20k max-t random triples (src/fast_simd.rs:1185-1236, :919-948)."""
+    img, pts = _ring_grid(512, 256, 7)             # 131072 rings per pass
+    checked = 0
+    for n in range(9, 17):                          # max-t: 8 x 131072
+        got = fast_hip.keypoint_scores(img, pts, Config(16, n, NonMaximalSuppression.MaxThreshold))
+        want = oracle.score_points(img, pts, 1, 16, n)
+        assert np.array_equal(got, want), n
+        checked += len(pts)
+    rng = np.random.default_rng(11)
+    order = rng.permutation(len(pts))
+    for t in range(256):                            # SAD: every threshold, 512 rings each
+        sel = pts[order[(t * 512) % len(pts):(t * 512) % len(pts) + 512]]
+        got = fast_hip.keypoint_scores(img, sel, Config(t, 9, NonMaximalSuppression.SumAbsolute))
+        assert np.array_equal(got, oracle.score_points(img, sel, 2, t, 9)), t
+        checked += len(sel)
+    for t in (0, 8, 16, 40):                        # SAD: all rings at the bench thresholds
+        got = fast_hip.keypoint_scores(img, pts, Config(t, 12, NonMaximalSuppression.SumAbsolute))
+        assert np.array_equal(got, oracle.score_points(img, pts, 2, t, 12)), t
+        checked += len(pts)
+    assert checked >= 1_000_000

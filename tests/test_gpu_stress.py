@@ -74,6 +74,17 @@ def mixed_batch():
 @pytest.mark.parametrize("nms", [0, 1, 2])
 @pytest.mark.parametrize("n", [9, 16])
 @pytest.mark.parametrize("t", [6, 20])
-def test_mixed_batch_full_geometry(mixed_batch, monkeypatch, t, n, nms):
-    monkeypatch.setenv("FDF_MIN_TASKS", "1")      # 64 frames with the full-size geometry
-    launch_twice_and_check(mixed_batch, t, n, nms, n_check=3)
+def test_mixed_batch_full_geometry(mixed_batch, t, n, nms):
+    ctx = fast_hip.context(0)
+    ctx.set_geometry(1)                           # 64 frames with the full-size geometry
+    try:
+        launch_twice_and_check(mixed_batch, t, n, nms, n_check=3)
+    finally:
+        ctx.set_geometry(0)
+
+
+def test_config4_exact_batch(s1_batch):
+    """BASELINE.json config 4's exact per-GPU workload: 512 S1 1080p frames, t=16 n=9,
+    max-t NMS -- launched twice (device-side equality), frame 0 and the 3 densest frames
+    against the oracle."""
+    launch_twice_and_check(s1_batch, 16, 9, 1, n_check=3)

@@ -95,7 +95,8 @@ def test_oracle_corner_matches_cyclic_helper():
 
 
 def test_sad_score_against_formula():
-    """src/fast_simd.rs:1185-1236 (test_score_function_3), on 200k random triples."""
+    """src/fast_simd.rs:1185-1236 (test_score_function_3), on 20k random triples (the GPU's
+    fdf_score_points gets 1M+ cases against the oracle in tests/test_gpu_scored.py)."""
     rng = np.random.default_rng(0)
     for _ in range(20000):
         ring = rng.integers(0, 256, 16)

@@ -12,7 +12,10 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+# the ablation switches exist only in the debug build (make debug)
+os.environ.setdefault("FDF_LIB_PATH", os.path.join(ROOT, "build", "libfdf_debug.so"))
 
 
 def main():
@@ -22,6 +25,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--threshold", type=int, default=16)
+    ap.add_argument("--count", type=int, default=9)
     ap.add_argument("--variants", default="maxt:0,maxt:2,maxt:3,off:0,off:2,off:3,sad:0")
     args = ap.parse_args()
     import torch
@@ -47,7 +52,7 @@ def main():
                     os.environ[name] = v[k]
                 else:
                     os.environ.pop(name, None)
-            cfg = Config(16, 9, NonMaximalSuppression(modes[mode]))
+            cfg = Config(args.threshold, args.count, NonMaximalSuppression(modes[mode]))
             fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
             s = torch.cuda.Event(enable_timing=True)
             e = torch.cuda.Event(enable_timing=True)

@@ -1,4 +1,6 @@
 #!/bin/bash
+# ablation switches live in the debug build only (make debug)
+export FDF_LIB_PATH=${FDF_LIB_PATH:-$(cd "$(dirname "$0")/.." && pwd)/build/libfdf_debug.so}
 # Timing of ablation variants (tools/ablate.py, interleaved rounds) plus one SQ instruction-mix
 # --pmc pass per variant.  Usage: tools/pmc_ablate.sh OUTDIR VARIANT,VARIANT,...
 O=$1; VS=$2

@@ -1,4 +1,6 @@
 #!/bin/bash
+# ablation switches live in the debug build only (make debug)
+export FDF_LIB_PATH=${FDF_LIB_PATH:-$(cd "$(dirname "$0")/.." && pwd)/build/libfdf_debug.so}
 # Read traffic of the detector kernel from request-size counters (bytes = 32/64/128 x the
 # requests of each size), for the normal run and for the row stream alone (full tests
 # disabled, FDF_DEBUG_FLAGS=1).  Usage: tools/traffic_bytes.sh OUTDIR [bench args]

@@ -1,4 +1,6 @@
 #!/bin/bash
+# ablation switches live in the debug build only (make debug)
+export FDF_LIB_PATH=${FDF_LIB_PATH:-$(cd "$(dirname "$0")/.." && pwd)/build/libfdf_debug.so}
 # Calibrates the PMC traffic of the detector kernel: FETCH_SIZE / WRITE_SIZE of the normal
 # run and of a run whose full tests are disabled (FDF_DEBUG_FLAGS=1: the row stream alone,
 # the access pattern the x2 FETCH_SIZE correction is calibrated for), plus the L2 hit rate.
