@@ -40,7 +40,6 @@ struct fdf_ctx {
     uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
-    uint8_t* d_map = nullptr;           size_t map_bytes = 0;      // NMS score map
     // cross-stream ordering: the device work of the last enqueue (on any stream) completes
     // at `done`; the next enqueue on another stream waits for it first
     hipEvent_t done = nullptr;
@@ -178,7 +177,6 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream) {
-    const uint32_t sb = fdfk::score_bytes_for(cfg->nms);
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms,
                                        ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks);
     const uint32_t R = geo.R;
@@ -207,10 +205,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     int rc;
     if ((rc = ensure(ctx, &ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), stream))) return rc;
     if ((rc = ensure(ctx, &ctx->d_counts, &ctx->counts_n, (size_t)ntasks, stream))) return rc;
-    // NMS score map: written at keypoints only and read only where the keypoint bitmap
-    // marks one, so it is never cleared
-    if (sb && (rc = ensure(ctx, &ctx->d_map, &ctx->map_bytes, (size_t)n_frames * w * h * sb, stream)))
-        return rc;
     fdfk::BandParams p;
     p.frames = d_frames;
     p.frame_stride = frame_stride;
@@ -227,7 +221,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.flags = flags;
     p.nstrips = geo.nstrips;
     p.nsub = geo.nsub;
-    p.scores = ctx->d_map;
     fdfk::CompactParams c;
     c.width = w;
     c.height = h;
@@ -494,7 +487,6 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_scores);
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
-        (void)hipFree(ctx->d_map);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         if (ctx->done) (void)hipEventDestroy(ctx->done);
         (void)hipStreamDestroy(ctx->stream);

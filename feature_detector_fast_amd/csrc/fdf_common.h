@@ -144,4 +144,24 @@ __device__ __forceinline__ uint32_t score_sum_abs(uint32_t c, const uint32_t (&p
     return max(sb, sd);
 }
 
+// The same SAD score from the packed ring (byte j of w[m] = circle pixel 4j + m) with
+// v_sad_u8 (per-byte |a - b| summed into an accumulator).  With U = min(c + t, 255) and
+// L = max(c - t, 0) (clamping changes no term: p <= 255, p >= 0) and max(x, 0) = (|x| + x) / 2:
+//   sum max(p - U, 0) = (sum |p - U| + sum p - 16 U) / 2
+//   sum max(L - p, 0) = (sum |p - L| - sum p + 16 L) / 2
+// -- 12 v_sad_u8 instead of ~100 unpack / sub / max / add operations.
+__device__ __forceinline__ uint32_t score_sum_abs_packed(uint32_t c, const uint32_t (&w)[4],
+                                                         uint32_t t) {
+    const uint32_t U = min(c + t, 255u), L = c > t ? c - t : 0u;
+    const uint32_t U4 = U * 0x01010101u, L4 = L * 0x01010101u;
+    uint32_t su = 0, sl = 0, sp = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        su = __builtin_amdgcn_sad_u8(w[m], U4, su);
+        sl = __builtin_amdgcn_sad_u8(w[m], L4, sl);
+        sp = __builtin_amdgcn_sad_u8(w[m], 0u, sp);
+    }
+    return max((su + sp - 16u * U) >> 1, (sl + 16u * L - sp) >> 1);
+}
+
 }  // namespace fdfk

@@ -134,8 +134,6 @@ struct BandParams {
     uint32_t* counts;            // ntasks keypoint counts (band order = raster order)
     uint32_t flags;              // kFlag* ablation switches, 0 in production
     uint32_t nstrips, nsub;      // sweep kernel: column strips x sub-bands per band
-    uint8_t* scores;             // NMS: score map, u8 (max-t) / u16 (SAD) per pixel, frame f at
-                                 // scores + f * width * height * score bytes (written at keypoints only)
 };
 
 // Bands per compaction workgroup: enough groups (~1024) to spread the copy over the chip.

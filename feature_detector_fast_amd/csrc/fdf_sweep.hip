@@ -117,7 +117,6 @@ struct UnitCtx {
     uint32_t head, tail;   // candidate FIFO: entries [head, tail) at pq[i % kSweepPixelQ]
     int ys;                // first row the unit sweeps (FIFO rows are relative to it)
     uint32_t flags;        // BandParams::flags (ablation runs only)
-    uint8_t* smap;         // NMS: this frame's score map
 };
 
 // ---------------------------------------------------------------------------------------
@@ -133,6 +132,20 @@ struct Batch {
     u32x2 a1, a5;          // rows y-2, y+2: 8 bytes from x-2
     u32x2 a2, a3, a4;      // rows y-1, y, y+1: 8 bytes from x-3
 };
+
+// The 7 row windows around centre (x, y) with o = (y - 3) * W + x.  They stay inside the
+// frame: rows y-3 .. y+3 are rows, and the 1-2 bytes past a row end (rows y-1 .. y+2 only)
+// belong to the next row.
+__device__ __forceinline__ void load_ring_windows(Batch& b, const __amdgpu_buffer_rsrc_t& rs,
+                                                  int o, int W) {
+    b.a0 = __builtin_amdgcn_raw_buffer_load_b32(rs, o - 1, 0, 0);
+    b.a1 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 2, W, 0));
+    b.a2 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 3, 2 * W, 0));
+    b.a3 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 3, 3 * W, 0));
+    b.a4 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 3, 4 * W, 0));
+    b.a5 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 2, 5 * W, 0));
+    b.a6 = __builtin_amdgcn_raw_buffer_load_b32(rs, o - 1, 6 * W, 0);
+}
 
 // Inclusive prefix sum over the wave's 64 lanes (DPP row shifts, then row broadcasts).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -237,15 +250,7 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             }
         }
     }
-    // the windows stay inside the frame: rows y-3 .. y+3 are rows, and the 1-2 bytes past
-    // a row end (rows y-1 .. y+2 only) belong to the next row
-    b.a0 = __builtin_amdgcn_raw_buffer_load_b32(u.src.rs, o - 1, 0, 0);
-    b.a1 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 2, W, 0));
-    b.a2 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 3, 2 * W, 0));
-    b.a3 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 3, 3 * W, 0));
-    b.a4 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 3, 4 * W, 0));
-    b.a5 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(u.src.rs, o - 2, 5 * W, 0));
-    b.a6 = __builtin_amdgcn_raw_buffer_load_b32(u.src.rs, o - 1, 6 * W, 0);
+    load_ring_windows(b, u.src.rs, o, W);
     return b;
 }
 
@@ -289,30 +294,27 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
     const bool is_kp = b.act && (kb || kd);
     if (is_kp) atomicOr(&sh.bitmap[(y - u.yb) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
     if constexpr (NMS != kNmsOff) {
-        // scores go to the band's LDS list; once it is full, to the frame's score map
+        // scores go to the band's LDS list; past its capacity they are only counted (the
+        // band NMS pass then ranks the listed ones into the band's slot and recomputes the
+        // rest from the frame)
         const uint64_t bal = wave_ballot(is_kp);
         if (bal) {
             uint32_t base = 0;
             if (u.lane == 0) base = atomicAdd(sh.slist_n, (uint32_t)__popcll(bal));
             base = __builtin_amdgcn_readfirstlane(base);
             if (is_kp) {
-                uint32_t p[16];
+                uint32_t score;
+                if constexpr (NMS == kNmsMaxThreshold) {
+                    uint32_t p[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
-#ifdef FDF_ABLATE_NO_SCORE   // timing ablation only: wrong NMS results
-                const uint32_t score = 1u + (p[0] & 1u);
-#else
-                const uint32_t score = NMS == kNmsMaxThreshold ? score_max_threshold<N>(c, p, kd)
-                                                               : score_sum_abs(c, p, u.t);
-#endif
-                const uint32_t idx = base + lanes_below(bal);
-                if (idx < sh.slist_cap) {
-                    sh.slist[idx] = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
+                    for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+                    score = score_max_threshold<N>(c, p, kd);
                 } else {
-                    const uint32_t o = (uint32_t)y * u.src.W + (uint32_t)x;
-                    if constexpr (NMS == kNmsMaxThreshold) u.smap[o] = (uint8_t)score;
-                    else reinterpret_cast<uint16_t*>(u.smap)[o] = (uint16_t)score;
+                    score = score_sum_abs_packed(c, w, u.t);
                 }
+                const uint32_t idx = base + lanes_below(bal);
+                if (idx < sh.slist_cap)
+                    sh.slist[idx] = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
             }
         }
     }
@@ -524,186 +526,6 @@ __device__ __forceinline__ uint32_t bits3(const uint32_t* row, int x) {
     return (uint32_t)(v >> sh) & 7u;
 }
 
-// Strict 3x3 maximum of one keypoint (src/fast_simd.rs:596-615): keep iff its score is above
-// the score of every neighbouring keypoint (non-keypoints score 0, ties suppress both).
-// `up`, `mid`, `dn`: neighbour bits of rows y-1, y, y+1 (bit k = column x-1+k).
-template <int NMS>
-__device__ __forceinline__ bool nms_keep(const __amdgpu_buffer_rsrc_t& map, uint32_t W, int x,
-                                         int y, uint32_t up, uint32_t mid, uint32_t dn) {
-    if ((up | mid | dn) == 0) return true;
-    const uint32_t o = (uint32_t)(y - 1) * W + (uint32_t)(x - 1);   // score of (x-1, y-1)
-    uint32_t s[3][3];
-    if constexpr (NMS == kNmsMaxThreshold) {
-        const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(map, o, 0, 0);
-        const uint32_t m = __builtin_amdgcn_raw_buffer_load_b32(map, o + W, 0, 0);
-        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(map, o + 2 * W, 0, 0);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            s[0][k] = (a >> (8 * k)) & 0xffu;
-            s[1][k] = (m >> (8 * k)) & 0xffu;
-            s[2][k] = (d >> (8 * k)) & 0xffu;
-        }
-    } else {
-        const u32x2 a = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * o, 0, 0));
-        const u32x2 m = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * (o + W), 0, 0));
-        const u32x2 d = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * (o + 2 * W), 0, 0));
-        s[0][0] = a.x & 0xffffu; s[0][1] = a.x >> 16; s[0][2] = a.y & 0xffffu;
-        s[1][0] = m.x & 0xffffu; s[1][1] = m.x >> 16; s[1][2] = m.y & 0xffffu;
-        s[2][0] = d.x & 0xffffu; s[2][1] = d.x >> 16; s[2][2] = d.y & 0xffffu;
-    }
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        mx = max(mx, (up >> k) & 1u ? s[0][k] : 0u);
-        mx = max(mx, (mid >> k) & 1u ? s[1][k] : 0u);
-        mx = max(mx, (dn >> k) & 1u ? s[2][k] : 0u);
-    }
-    return s[1][1] > mx;
-}
-
-// Pass 1 of band_nms: the band's keypoints that have a neighbouring keypoint, as
-// r * W + x (band row r), into list[0 .. cap); returns how many there are (even past cap).
-__device__ __forceinline__ uint32_t nms_collect(const uint32_t* bitmap, uint32_t nwords,
-                                                uint32_t nw, uint32_t W, uint32_t* list,
-                                                uint32_t cap, uint32_t* list_n) {
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) *list_n = 0;
-    __syncthreads();
-    for (uint32_t w = tid; w < nwords; w += kThreads) {
-        const uint32_t r = w / nw;                       // band row; bitmap row r + 1
-        uint32_t bits = bitmap[w + nw];
-        const uint32_t* above = bitmap + r * nw;
-        while (bits) {
-            const uint32_t bit = __builtin_ctz(bits);
-            bits &= bits - 1;
-            const int x = (int)((w - r * nw) * 32 + bit);
-            if ((bits3(above, x) | (bits3(above + nw, x) & 5u) | bits3(above + 2 * nw, x)) == 0)
-                continue;
-            const uint32_t i = atomicAdd(list_n, 1u);
-            if (i < cap) list[i] = r * W + (uint32_t)x;
-        }
-    }
-    __syncthreads();
-    const uint32_t n = *list_n;
-    // every wave has its count before a second call (band_nms) resets it
-    __syncthreads();
-    return n;
-}
-
-// Pass 2 + 3 of band_nms on a complete list (LDS or global): compare, then clear.
-template <int NMS>
-__device__ __forceinline__ void nms_listed(uint32_t* bitmap, uint32_t nw, uint32_t y0,
-                                           uint32_t W, const __amdgpu_buffer_rsrc_t& map,
-                                           uint32_t* list, uint32_t n_list) {
-    constexpr int kNmsUnroll = 4;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t i0 = tid; i0 < n_list; i0 += kNmsUnroll * kThreads) {
-        u32x2 s[kNmsUnroll][3];     // scores of columns x-1 .. x+1, rows y-1 .. y+1
-        int xs[kNmsUnroll], rs[kNmsUnroll];
-#pragma unroll
-        for (int k = 0; k < kNmsUnroll; ++k) {
-            const uint32_t i = i0 + k * kThreads;
-            const uint32_t e = i < n_list ? list[i] : W + 3u;   // inactive: a harmless centre
-            rs[k] = (int)(e / W);
-            xs[k] = (int)(e - (uint32_t)rs[k] * W);
-            const uint32_t o = (y0 + rs[k] - 1) * W + (uint32_t)xs[k] - 1;   // (x-1, y-1)
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                if constexpr (NMS == kNmsMaxThreshold)
-                    s[k][d].x = __builtin_amdgcn_raw_buffer_load_b32(map, o + d * W, 0, 0);
-                else
-                    s[k][d] = __builtin_bit_cast(
-                        u32x2, __builtin_amdgcn_raw_buffer_load_b64(map, 2 * (o + d * W), 0, 0));
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kNmsUnroll; ++k) {
-            const uint32_t i = i0 + k * kThreads;
-            if (i < n_list) {
-                const int x = xs[k];
-                const uint32_t* above = bitmap + rs[k] * nw;
-                const uint32_t nb[3] = {bits3(above, x), bits3(above + nw, x) & 5u,
-                                        bits3(above + 2 * nw, x)};
-                uint32_t mx = 0, own = 0;
-#pragma unroll
-                for (int d = 0; d < 3; ++d) {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        uint32_t v;
-                        if constexpr (NMS == kNmsMaxThreshold)
-                            v = (s[k][d].x >> (8 * c)) & 0xffu;
-                        else
-                            v = c == 2 ? (s[k][d].y & 0xffffu) : (s[k][d].x >> (16 * c)) & 0xffffu;
-                        if (d == 1 && c == 1) own = v;
-                        mx = max(mx, (nb[d] >> c) & 1u ? v : 0u);
-                    }
-                }
-                if (own <= mx) list[i] |= 0x80000000u;   // suppressed
-            }
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < n_list; i += kThreads) {
-        const uint32_t e = list[i];
-        if (e & 0x80000000u) {
-            const uint32_t v = e & 0x7fffffffu, r = v / W, x = v - r * W;
-            atomicAnd(&bitmap[(r + 1) * nw + (x >> 5)], ~(1u << (x & 31)));
-        }
-    }
-}
-
-// Band NMS (src/fast_simd.rs:589-616) in place on the keypoint bitmap: bitmap row 0 and
-// rows + 1 are the rows just outside the band (neighbours only).  Keypoints without
-// neighbouring keypoints are kept outright.  The others are listed -- in LDS (`lds_list`,
-// the FIFO area, free now), or when that is too small in the band's output slot
-// (`scratch`) -- and compared with their neighbours' scores from the score map, kNmsUnroll
-// per thread with all their loads in flight together; the suppressed ones are cleared once
-// every comparison has read the bitmap.  A band with more such keypoints than the slot holds
-// (dense images) computes its keep-bits word by word into the slot and copies them back.
-// Rows 3 and h-4 are never output (:590-592, :342).
-template <int NMS>
-__device__ void band_nms(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
-                         uint32_t H, uint8_t* smap, uint32_t* lds_list, uint32_t lds_cap,
-                         uint32_t* list_n, uint32_t* scratch, uint32_t scratch_cap) {
-    constexpr uint32_t sbytes = NMS == kNmsSumAbsolute ? 2u : 1u;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t nwords = rows * nw;
-    const __amdgpu_buffer_rsrc_t map =
-        __builtin_amdgcn_make_buffer_rsrc(smap, 0, (int)(W * H * sbytes), 0x00020000);
-    uint32_t n = nms_collect(bitmap, nwords, nw, W, lds_list, lds_cap, list_n);
-    if (n <= lds_cap) {
-        nms_listed<NMS>(bitmap, nw, y0, W, map, lds_list, n);
-    } else if (n <= scratch_cap) {
-        n = nms_collect(bitmap, nwords, nw, W, scratch, scratch_cap, list_n);
-        nms_listed<NMS>(bitmap, nw, y0, W, map, scratch, n);
-    } else {
-        // dense band: keep-bits word by word (serial score loads), via the slot
-        for (uint32_t w = tid; w < nwords; w += kThreads) {
-            const uint32_t r = w / nw;
-            uint32_t bits = bitmap[w + nw], kept = bits;
-            const uint32_t* above = bitmap + r * nw;
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
-                const int x = (int)((w - r * nw) * 32 + bit);
-                if (!nms_keep<NMS>(map, W, x, (int)(y0 + r), bits3(above, x),
-                                   bits3(above + nw, x) & 5u, bits3(above + 2 * nw, x)))
-                    kept &= ~(1u << bit);
-            }
-            scratch[w] = kept;
-        }
-        __syncthreads();
-        for (uint32_t w = tid; w < nwords; w += kThreads) bitmap[w + nw] = scratch[w];
-    }
-    __syncthreads();
-    // rows 3 and h - 4 keep no keypoints (they were neighbours only)
-    for (uint32_t y : {3u, H - 4u}) {
-        if (y < y0 || y >= y0 + rows) continue;
-        for (uint32_t w = tid; w < nw; w += kThreads) bitmap[(y - y0 + 1) * nw + w] = 0;
-    }
-    __syncthreads();
-}
-
 // Raster rank of bitmap position (row, x): keypoints before it in the band's bitmap.
 // rprefix[row] counts the rows above, bprefix[row * nb + k] the words [0, 4k) of the row.
 __device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const uint16_t* bprefix,
@@ -721,18 +543,23 @@ __device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const ui
     return r + __popc(rw[wi] & ((1u << (x & 31)) - 1u));
 }
 
-// Band NMS (src/fast_simd.rs:589-616) from the LDS score list, in place on the keypoint
-// bitmap (bitmap rows 0 and rows + 1 are the rows just outside the band, neighbours only).
-// The list holds every keypoint of the bitmap once; its scores are scattered into raster
-// rank order, then each keypoint of the band's own rows reads its neighbours' scores by
-// rank, and the suppressed ones are cleared once every comparison has read the bitmap.
-// Rows 3 and h-4 are never output (:590-592, :342).
-template <int NMS>
-__device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
-                             uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
-                             uint16_t* bprefix, uint32_t* rprefix, uint32_t flags) {
+// Neighbour bits of bitmap position (row, x) among the R2 bitmap rows: bit k of the up /
+// down rows = column x-1+k, mid row bits 0 and 2 (columns x-1, x+1).  Non-zero iff the
+// keypoint has a neighbouring keypoint.
+__device__ __forceinline__ uint32_t neighbour_bits(const uint32_t* bitmap, uint32_t nw, uint32_t R2,
+                                                   uint32_t row, uint32_t x) {
+    return (row > 0 ? bits3(bitmap + (row - 1) * nw, (int)x) : 0u) |
+           (bits3(bitmap + row * nw, (int)x) & 5u) |
+           (row + 1 < R2 ? bits3(bitmap + (row + 1) * nw, (int)x) : 0u);
+}
+
+// Rank prefixes of the band's keypoint bitmap (R2 rows): rprefix[row] = keypoints in the
+// rows above, bprefix[row * nb + k] = keypoints in words [0, 4k) of the row.  Returns the
+// bitmap's keypoint total (every thread).
+__device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint32_t nw,
+                                       uint16_t* bprefix, uint32_t* rprefix, uint32_t* total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    const uint32_t nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
     if (nb_blocks <= 16) {
         // one bitmap row per 16-lane DPP row: lane k counts block k, a row_shr scan turns the
         // counts into the row's block prefixes and lane 15 ends with the row total
@@ -788,17 +615,31 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
             if (base + lane < R2) rprefix[base + lane] = carry + incl - v;
             carry += __shfl(incl, 63, 64);
         }
+        if (lane == 0) *total = carry;
     }
     __syncthreads();
+    return *total;
+}
+
+// Band NMS (src/fast_simd.rs:589-616) from the LDS score list, in place on the keypoint
+// bitmap (bitmap rows 0 and rows + 1 are the rows just outside the band, neighbours only).
+// The list holds every keypoint of the bitmap once; its scores are scattered into raster
+// rank order, then each keypoint of the band's own rows reads its neighbours' scores by
+// rank, and the suppressed ones are cleared once every comparison has read the bitmap.
+// Rows 3 and h-4 are never output (:590-592, :342).
+template <int NMS>
+__device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                             uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
+                             uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
     if (flags & kFlagNmsPrefixOnly) return;
     // scores of keypoints with a neighbouring keypoint into rank order (the others' scores are
     // never read: an isolated keypoint is kept, and marked by a zero score field)
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
-        const uint32_t nb = bits3(bitmap + (row - 1 + (row == 0)) * nw, (int)x) * (row != 0) |
-                            (bits3(bitmap + row * nw, (int)x) & 5u) |
-                            (row + 1 < R2 ? bits3(bitmap + (row + 1) * nw, (int)x) : 0u);
-        if (nb == 0) slist[i] = e & ~0xfffu;
+        if (neighbour_bits(bitmap, nw, R2, row, x) == 0) slist[i] = e & ~0xfffu;
         else sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
     }
     __syncthreads();
@@ -841,6 +682,156 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
             const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
             atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
         }
+    }
+    __syncthreads();
+}
+
+// Score of the keypoint at (x, y) recomputed from the frame (the same windows, packing and
+// score functions as the sweep's full test).
+template <int NMS, int N>
+__device__ __forceinline__ uint32_t keypoint_score(const __amdgpu_buffer_rsrc_t& rs, int W, int x,
+                                                   int y, const LerpConsts& lk, uint32_t t) {
+    Batch b;
+    load_ring_windows(b, rs, (y - 3) * W + x, W);
+    uint32_t w[4], c;
+    pack_ring(b, w, c);
+    if constexpr (NMS == kNmsSumAbsolute) {
+        return score_sum_abs_packed(c, w, t);
+    } else {
+        bool kb, kd;
+        lane_segment_test_packed<N>(c, w, lk, kb, kd);
+        uint32_t p[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+        return score_max_threshold<N>(c, p, kd);
+    }
+}
+
+// Band NMS when the band has more keypoints than the LDS score list holds (dense images).
+// The band's output slot is scratch until the band writes its result:
+//  * when 2 bytes per bitmap keypoint fit in the slot, the slot holds every score in raster
+//    rank order: the listed scores are scattered there, the keypoints that take part in a
+//    comparison (those with a neighbouring keypoint) and were not listed get their score
+//    recomputed from the frame, each keypoint of the band's rows compares its score with its
+//    neighbours' (marking the suppressed ones in the score's top bit), and each thread then
+//    clears the marked keypoints of whole bitmap rows (ranks only depend on their own row and
+//    the row prefixes, so rows can change independently);
+//  * otherwise (more keypoints than slot bytes / 2) no scores are stored: each keypoint with a
+//    neighbouring keypoint recomputes its own and its neighbours' scores, the kill masks go
+//    to the slot (one word per bitmap word, exactly the slot's size) and are applied after.
+// Rows 3 and h-4 are never output (:590-592, :342); the caller clears them.
+template <int NMS, int N>
+__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                               uint32_t H, const uint32_t* slist, uint32_t n_list,
+                               uint16_t* bprefix, uint32_t* rprefix, uint32_t* total,
+                               uint32_t* slot, uint32_t slot_bytes,
+                               const __amdgpu_buffer_rsrc_t& frame, const LerpConsts& lk, uint32_t t) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    const uint32_t K = band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
+    constexpr uint16_t kUnset = 0x7fffu, kMark = 0x8000u;
+    if (2ull * K <= slot_bytes) {
+        uint16_t* sr = reinterpret_cast<uint16_t*>(slot);
+        for (uint32_t i = tid; i < K; i += kThreads) sr[i] = kUnset;
+        __syncthreads();
+        for (uint32_t i = tid; i < n_list; i += kThreads) {
+            const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
+            if (neighbour_bits(bitmap, nw, R2, row, x))
+                sr[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
+        }
+        __syncthreads();
+        for (uint32_t wi = tid; wi < R2 * nw; wi += kThreads) {   // unlisted: recompute
+            const uint32_t row = wi / nw;
+            uint32_t bits = bitmap[wi];
+            while (bits) {
+                const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
+                bits &= bits - 1;
+                if (!neighbour_bits(bitmap, nw, R2, row, x)) continue;
+                const uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+                if (sr[r] == kUnset)
+                    sr[r] = (uint16_t)keypoint_score<NMS, N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), lk, t);
+            }
+        }
+        __syncthreads();
+        for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {   // compare
+            const uint32_t row = wi / nw;
+            uint32_t bits = bitmap[wi];
+            while (bits) {
+                const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t mid = bits3(bitmap + row * nw, (int)x);
+                const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
+                const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
+                if (((mid & 5u) | up | dn) == 0) continue;
+                const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+                const uint32_t own = sr[ro] & 0x7fffu;
+                uint32_t mx = 0;
+                if (mid & 1u) mx = max(mx, sr[ro - 1] & 0x7fffu);
+                if (mid & 4u) mx = max(mx, sr[ro + 1] & 0x7fffu);
+#pragma unroll
+                for (int d = -1; d <= 1; d += 2) {
+                    const uint32_t nbits = d < 0 ? up : dn;
+                    if (nbits) {
+                        uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            if ((nbits >> k) & 1u) {
+                                mx = max(mx, sr[r] & 0x7fffu);
+                                ++r;
+                            }
+                        }
+                    }
+                }
+                if (own <= mx) sr[ro] = (uint16_t)(own | kMark);
+            }
+        }
+        __syncthreads();
+        for (uint32_t row = 1 + tid; row + 1 < R2; row += kThreads) {   // clear, row by row
+            uint32_t r = rprefix[row];
+            uint32_t* rw = bitmap + row * nw;
+            for (uint32_t k = 0; k < nw; ++k) {
+                const uint32_t v = rw[k];
+                uint32_t bits = v, kill = 0;
+                while (bits) {
+                    const uint32_t bit = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    if (sr[r] & kMark) kill |= 1u << bit;
+                    ++r;
+                }
+                if (kill) rw[k] = v & ~kill;
+            }
+        }
+    } else {
+        for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {
+            const uint32_t row = wi / nw;
+            uint32_t bits = bitmap[wi], kill = 0;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t x = (wi - row * nw) * 32 + bit;
+                const int y = (int)(y0 - 1 + row);
+                const uint32_t mid = bits3(bitmap + row * nw, (int)x) & 5u;
+                const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
+                const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
+                if ((mid | up | dn) == 0) continue;
+                const uint32_t own = keypoint_score<NMS, N>(frame, (int)W, (int)x, y, lk, t);
+                bool suppressed = false;
+#pragma unroll
+                for (int d = -1; d <= 1; ++d) {
+                    const uint32_t nbits = d < 0 ? up : (d == 0 ? mid : dn);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        if (!suppressed && ((nbits >> k) & 1u) &&
+                            keypoint_score<NMS, N>(frame, (int)W, (int)x - 1 + k, y + d, lk, t) >= own)
+                            suppressed = true;
+                    }
+                }
+                if (suppressed) kill |= 1u << bit;
+            }
+            slot[wi - nw] = kill;
+        }
+        __syncthreads();
+        for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) bitmap[wi] &= ~slot[wi - nw];
     }
     __syncthreads();
 }
@@ -921,8 +912,6 @@ void fast_sweep_kernel(BandParams P) {
         const_cast<uint8_t*>(img), 0, (int)(W * H + 15), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_exact = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(img), 0, (int)(W * H), 0x00020000);
-    constexpr uint32_t sbytes = NMS == kNmsSumAbsolute ? 2u : 1u;
-    u.smap = P.scores + (uint64_t)frame * W * H * sbytes;
     u.t = P.threshold;
     u.nw = nw;
     u.yb = (int)(y0 - halo);
@@ -973,20 +962,21 @@ void fast_sweep_kernel(BandParams P) {
             band_nms_lds<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, n,
                               reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                               reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), ablation_flags(P.flags));
+                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+                              ablation_flags(P.flags));
         } else {
-            // more keypoints than the list holds: the listed scores join the score map
-            for (uint32_t i = tid; i < sh.slist_cap; i += kThreads) {
-                const uint32_t e = sh.slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
-                const uint32_t o = (y0 - 1 + row) * W + x;
-                if constexpr (NMS == kNmsMaxThreshold) u.smap[o] = (uint8_t)(e & 0xfffu);
-                else reinterpret_cast<uint16_t*>(u.smap)[o] = (uint16_t)(e & 0xfffu);
+            // more keypoints than the list holds: the band's slot is the scratch
+            band_nms_spill<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap,
+                                   reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                                   reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+                                   reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
+                                   P.slot_bytes, rs_exact, lk, P.threshold);
+            // rows 3 and h - 4 keep no keypoints (they were neighbours only)
+            for (uint32_t y : {3u, H - 4u}) {
+                if (y < y0 || y >= y0 + rows) continue;
+                for (uint32_t w = tid; w < nw; w += kThreads) bitmap[(y - y0 + 1) * nw + w] = 0;
             }
             __syncthreads();
-            band_nms<NMS>(bitmap, rows, nw, y0, W, H, u.smap,
-                          reinterpret_cast<uint32_t*>(smem_raw + L.pq), kWaves * L.wave_bytes / 4,
-                          unit_ctr + 2, reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
-                          P.slot_bytes / 4);
         }
         // the band's own rows are now its keep-bits
     }

@@ -359,3 +359,41 @@ def test_cli_helpers_without_gpu(tmp_path):
     assert f.read_text() == "3 4\n0 5\n10 8\n"
     assert np.array_equal(workloads.read_points(str(f)), pts)
     assert cli.main(["--help"]) == 0
+
+
+def _sad_u8(a, b, acc):
+    """v_sad_u8: acc + sum over the 4 bytes of |a.byte - b.byte| (uint32 arrays)."""
+    tot = acc.astype(np.int64)
+    for k in range(4):
+        tot += np.abs(((a >> (8 * k)) & 0xFF).astype(np.int64) - ((b >> (8 * k)) & 0xFF).astype(np.int64))
+    return tot.astype(np.uint32)
+
+
+def test_sad_score_packed_identity():
+    """fdf_common.h score_sum_abs_packed: the SAD score from 12 v_sad_u8 on the packed ring
+    equals the reference's SAD score (src/opencv_compat.rs:278-299) for random rings, all t,
+    including the saturating ends (c + t > 255, c < t)."""
+    rng = np.random.default_rng(5)
+    m = 200000
+    ring = rng.integers(0, 256, (m, 16)).astype(np.int64)
+    c = rng.integers(0, 256, m).astype(np.int64)
+    near = rng.integers(0, 2, m).astype(bool)          # half the rings close to the centre
+    ring[near] = np.clip(c[near, None] + rng.integers(-30, 31, (near.sum(), 16)), 0, 255)
+    t = rng.integers(0, 256, m).astype(np.int64)
+    w = [np.zeros(m, dtype=np.uint32) for _ in range(4)]
+    for i in range(16):                                 # byte j of w[k] = pixel 4j + k
+        w[i & 3] |= (ring[:, i].astype(np.uint32) << np.uint32(8 * (i >> 2)))
+    U = np.minimum(c + t, 255).astype(np.uint32)
+    L = np.where(c > t, c - t, 0).astype(np.uint32)
+    su = sl = sp = np.zeros(m, dtype=np.uint32)
+    for k in range(4):
+        su = _sad_u8(w[k], U * np.uint32(0x01010101), su)
+        sl = _sad_u8(w[k], L * np.uint32(0x01010101), sl)
+        sp = _sad_u8(w[k], np.zeros(m, dtype=np.uint32), sp)
+    su, sl, sp = su.astype(np.int64), sl.astype(np.int64), sp.astype(np.int64)
+    got = np.maximum((su + sp - 16 * U) >> 1, (sl + 16 * L - sp) >> 1)
+    sb = np.maximum(ring - (c + t)[:, None], 0).sum(1)
+    sd = np.maximum((c - t)[:, None] - ring, 0).sum(1)
+    assert np.array_equal(got, np.maximum(sb, sd))
+    for k in range(0, m, 20000):                        # and the literal oracle, sampled
+        assert got[k] == oracle.score_sum_abs(int(c[k]), ring[k].tolist(), int(t[k]))
