@@ -66,21 +66,24 @@ constexpr int kSweepWavesPerEU = FDF_WAVES_PER_EU;
 // neighbouring bands' rows, so the band also tests one row each side (scores only).
 __host__ __device__ inline uint32_t band_halo(uint32_t nms) { return nms ? 1u : 0u; }
 
-// LDS of one workgroup: 4 candidate FIFOs (+ batch staging) and the keypoint bitmap of the band's R rows plus
-// the NMS halo rows (NMS then clears the suppressed keypoints in place; one pad word after
-// the bitmap lets bit look-ups read two words unconditionally).  NMS also keeps the band's
-// keypoint scores: a list of kScoreListCap (position, score) entries and per-row /
-// per-4-word-block keypoint counts that turn a bitmap position into its raster rank; the
-// scores in rank order go to the FIFO area once the sweep is done.
+// LDS of one workgroup: the keypoint bitmap of the band's R rows plus the NMS halo rows (NMS
+// then clears the suppressed keypoints in place; one pad word after the bitmap lets bit
+// look-ups read two words unconditionally), 4 candidate FIFOs (+ batch staging), and for NMS
+// the band's keypoint scores: a list of kScoreListCap (position, score) entries and per-row /
+// per-4-word-block keypoint counts that turn a bitmap position into its raster rank.  The
+// FIFOs, staging and score list are contiguous: once the sweep is done they hold the scores
+// in rank order (`nms_area`, u16 entries; the FIFO part alone for band_nms_lds).
 #ifndef FDF_SLIST_CAP
 #define FDF_SLIST_CAP 2048
 #endif
 constexpr uint32_t kScoreListCap = FDF_SLIST_CAP;
+constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix block
 // band_nms_lds ranks the list's scores as u16 into the 4 candidate FIFOs
 static_assert(kScoreListCap * 2 <= 4 * kSweepPixelQ * 4, "ranked scores must fit the FIFO area");
-constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix block
+static_assert(kScoreListCap % 256 == 0, "the spill NMS pass holds the list 1/256 per thread");
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
+    uint32_t nms_area_entries;   // u16 ranked scores that fit [pq, bprefix) after the sweep
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t v);
@@ -89,13 +92,14 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     SweepLayout L;
     const uint32_t rows = R + 2 * band_halo(nms);
     const uint32_t nb = (nw + kRankBlock - 1) / kRankBlock;
-    L.pq = 0;
+    L.bitmap = 0;
+    L.pq = align16(rows * nw * 4 + 4);
     L.wave_bytes = kSweepPixelQ * 4;              // 4 FIFOs = kScoreListCap u16 ranked scores
-    L.stage = 4 * L.wave_bytes;                   // 4 x 64 staged batch pixels
-    L.bitmap = L.stage + 4 * 64 * 4;
-    L.slist = L.bitmap + align16(rows * nw * 4 + 4);
+    L.stage = L.pq + 4 * L.wave_bytes;            // 4 x 64 staged batch pixels
+    L.slist = L.stage + 4 * 64 * 4;
     const uint32_t cap = nms ? kScoreListCap : 0u;
     L.bprefix = L.slist + cap * 4;
+    L.nms_area_entries = (L.bprefix - L.pq) / 2;
     L.rprefix = L.bprefix + (nms ? align16(rows * nb * 2) : 0u);
     L.misc = L.rprefix + (nms ? align16(rows * 4) : 0u);
     L.total = L.misc + 64;

@@ -103,7 +103,7 @@ struct SweepShared {
     uint32_t* stage;       // 64 pixels of the batch being issued: (row - ys) << 10 | strip column
     uint32_t* bitmap;      // band keypoints: bitmap row i = image row yb + i, words_per_row each
     uint32_t* slist;       // NMS: the band's keypoints as (bitmap row * W + x) << 12 | score
-    uint32_t* slist_n;     // entries appended (past slist_cap: the rest went to the map)
+    uint32_t* slist_n;     // entries appended (past slist_cap only counted)
     uint32_t slist_cap;    // kScoreListCap, or 0 when a position does not fit 20 bits
 };
 
@@ -707,100 +707,135 @@ __device__ __forceinline__ uint32_t keypoint_score(const __amdgpu_buffer_rsrc_t&
     }
 }
 
-// Band NMS when the band has more keypoints than the LDS score list holds (dense images).
-// The band's output slot is scratch until the band writes its result:
-//  * when 2 bytes per bitmap keypoint fit in the slot, the slot holds every score in raster
-//    rank order: the listed scores are scattered there, the keypoints that take part in a
-//    comparison (those with a neighbouring keypoint) and were not listed get their score
-//    recomputed from the frame, each keypoint of the band's rows compares its score with its
-//    neighbours' (marking the suppressed ones in the score's top bit), and each thread then
-//    clears the marked keypoints of whole bitmap rows (ranks only depend on their own row and
-//    the row prefixes, so rows can change independently);
-//  * otherwise (more keypoints than slot bytes / 2) no scores are stored: each keypoint with a
-//    neighbouring keypoint recomputes its own and its neighbours' scores, the kill masks go
-//    to the slot (one word per bitmap word, exactly the slot's size) and are applied after.
-// Rows 3 and h-4 are never output (:590-592, :342); the caller clears them.
+// Band NMS over ranked scores `sr` (u16 per bitmap keypoint, raster rank order; LDS or the
+// band's slot), for a band whose score list overflowed.  `ent` holds this thread's share of
+// the list (kScoreListCap / kThreads entries, ~0 = none):
+//  1. every rank is set to kUnset and the listed scores are scattered to their ranks;
+//  2. keypoints that take part in a comparison (those with a neighbouring keypoint) and were
+//     not listed get their score recomputed from the frame;
+//  3. each keypoint of the band's rows compares its score with its neighbours', marking the
+//     suppressed ones in the score's top bit;
+//  4. one wave per bitmap row clears the marked keypoints (lane = word, ranks from a wave
+//     scan of the row's original words; a row's ranks only depend on that row and the row
+//     prefixes, so rows can change independently).
+constexpr uint32_t kSpillPer = kScoreListCap / kThreads;
+constexpr uint16_t kUnset = 0x7fffu, kMark = 0x8000u;
+
 template <int NMS, int N>
-__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
-                               uint32_t H, const uint32_t* slist, uint32_t n_list,
-                               uint16_t* bprefix, uint32_t* rprefix, uint32_t* total,
-                               uint32_t* slot, uint32_t slot_bytes,
-                               const __amdgpu_buffer_rsrc_t& frame, const LerpConsts& lk, uint32_t t) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
-    const uint32_t K = band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
-    constexpr uint16_t kUnset = 0x7fffu, kMark = 0x8000u;
-    if (2ull * K <= slot_bytes) {
-        uint16_t* sr = reinterpret_cast<uint16_t*>(slot);
-        for (uint32_t i = tid; i < K; i += kThreads) sr[i] = kUnset;
-        __syncthreads();
-        for (uint32_t i = tid; i < n_list; i += kThreads) {
-            const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
-            if (neighbour_bits(bitmap, nw, R2, row, x))
-                sr[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
-        }
-        __syncthreads();
-        for (uint32_t wi = tid; wi < R2 * nw; wi += kThreads) {   // unlisted: recompute
-            const uint32_t row = wi / nw;
-            uint32_t bits = bitmap[wi];
-            while (bits) {
-                const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
-                bits &= bits - 1;
-                if (!neighbour_bits(bitmap, nw, R2, row, x)) continue;
-                const uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
-                if (sr[r] == kUnset)
-                    sr[r] = (uint16_t)keypoint_score<NMS, N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), lk, t);
-            }
-        }
-        __syncthreads();
-        for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {   // compare
-            const uint32_t row = wi / nw;
-            uint32_t bits = bitmap[wi];
-            while (bits) {
-                const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t mid = bits3(bitmap + row * nw, (int)x);
-                const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
-                const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
-                if (((mid & 5u) | up | dn) == 0) continue;
-                const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
-                const uint32_t own = sr[ro] & 0x7fffu;
-                uint32_t mx = 0;
-                if (mid & 1u) mx = max(mx, sr[ro - 1] & 0x7fffu);
-                if (mid & 4u) mx = max(mx, sr[ro + 1] & 0x7fffu);
+__device__ __forceinline__ void nms_ranked(uint16_t* sr, const uint32_t (&ent)[kSpillPer],
+                                           uint32_t K, uint32_t* bitmap, uint32_t R2, uint32_t nw,
+                                           uint32_t y0, uint32_t W, const uint16_t* bprefix,
+                                           const uint32_t* rprefix,
+                                           const __amdgpu_buffer_rsrc_t& frame,
+                                           const LerpConsts& lk, uint32_t t) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    for (uint32_t i = tid; i < K; i += kThreads) sr[i] = kUnset;
+    __syncthreads();
 #pragma unroll
-                for (int d = -1; d <= 1; d += 2) {
-                    const uint32_t nbits = d < 0 ? up : dn;
-                    if (nbits) {
-                        uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
+    for (uint32_t j = 0; j < kSpillPer; ++j) {
+        const uint32_t e = ent[j];
+        if (e == ~0u) continue;
+        const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+        if (neighbour_bits(bitmap, nw, R2, row, x))
+            sr[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
+    }
+    __syncthreads();
+    for (uint32_t wi = tid; wi < R2 * nw; wi += kThreads) {   // unlisted: recompute
+        const uint32_t row = wi / nw;
+        uint32_t bits = bitmap[wi];
+        while (bits) {
+            const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
+            bits &= bits - 1;
+            if (!neighbour_bits(bitmap, nw, R2, row, x)) continue;
+            const uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+            if (sr[r] == kUnset)
+                sr[r] = (uint16_t)keypoint_score<NMS, N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), lk, t);
+        }
+    }
+    __syncthreads();
+    for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {   // compare
+        const uint32_t row = wi / nw;
+        uint32_t bits = bitmap[wi];
+        while (bits) {
+            const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
+            bits &= bits - 1;
+            const uint32_t mid = bits3(bitmap + row * nw, (int)x);
+            const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
+            const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
+            if (((mid & 5u) | up | dn) == 0) continue;
+            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+            const uint32_t own = sr[ro] & 0x7fffu;
+            uint32_t mx = 0;
+            if (mid & 1u) mx = max(mx, sr[ro - 1] & 0x7fffu);
+            if (mid & 4u) mx = max(mx, sr[ro + 1] & 0x7fffu);
 #pragma unroll
-                        for (int k = 0; k < 3; ++k) {
-                            if ((nbits >> k) & 1u) {
-                                mx = max(mx, sr[r] & 0x7fffu);
-                                ++r;
-                            }
+            for (int d = -1; d <= 1; d += 2) {
+                const uint32_t nbits = d < 0 ? up : dn;
+                if (nbits) {
+                    uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        if ((nbits >> k) & 1u) {
+                            mx = max(mx, sr[r] & 0x7fffu);
+                            ++r;
                         }
                     }
                 }
-                if (own <= mx) sr[ro] = (uint16_t)(own | kMark);
             }
+            if (own <= mx) sr[ro] = (uint16_t)(own | kMark);
         }
-        __syncthreads();
-        for (uint32_t row = 1 + tid; row + 1 < R2; row += kThreads) {   // clear, row by row
-            uint32_t r = rprefix[row];
-            uint32_t* rw = bitmap + row * nw;
-            for (uint32_t k = 0; k < nw; ++k) {
-                const uint32_t v = rw[k];
-                uint32_t bits = v, kill = 0;
-                while (bits) {
-                    const uint32_t bit = __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    if (sr[r] & kMark) kill |= 1u << bit;
-                    ++r;
-                }
-                if (kill) rw[k] = v & ~kill;
+    }
+    __syncthreads();
+    for (uint32_t row = 1 + wave; row + 1 < R2; row += kWaves) {   // clear
+        uint32_t* rw = bitmap + row * nw;
+        uint32_t carry = rprefix[row];
+        for (uint32_t k0 = 0; k0 < nw; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const uint32_t v = k < nw ? rw[k] : 0u;
+            const uint32_t c = __popc(v);
+            const uint32_t incl = wave_incl_scan(c);
+            uint32_t r = carry + incl - c, bits = v, kill = 0;
+            carry += __builtin_amdgcn_readlane(incl, 63);
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                if (sr[r] & kMark) kill |= 1u << bit;
+                ++r;
             }
+            if (kill) rw[k] = v & ~kill;
         }
+    }
+}
+
+// Band NMS when the band has more keypoints than the LDS score list holds (dense images):
+// with K keypoints in the band's bitmap, the ranked scores go to the LDS area the FIFOs,
+// staging and list occupied during the sweep (K <= lds_cap; the list is first moved to
+// registers), else to the band's output slot, which is scratch until the band writes its
+// result (2 K <= slot bytes), see nms_ranked.  A band denser still stores no scores: each
+// keypoint with a neighbouring keypoint recomputes its own and its neighbours' scores, the
+// kill masks go to the slot (one word per bitmap word, exactly the slot's size) and are
+// applied after.  Rows 3 and h-4 are never output (:590-592, :342); the caller clears them.
+template <int NMS, int N>
+__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                               uint32_t H, const uint32_t* slist, uint32_t n_list, uint16_t* lds_area,
+                               uint32_t lds_cap, uint16_t* bprefix, uint32_t* rprefix,
+                               uint32_t* total, uint32_t* slot, uint32_t slot_bytes,
+                               const __amdgpu_buffer_rsrc_t& frame, const LerpConsts& lk, uint32_t t) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2;
+    const uint32_t K = band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
+    if (K <= lds_cap || 2ull * K <= slot_bytes) {
+        uint32_t ent[kSpillPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kSpillPer; ++j)
+            ent[j] = tid + j * kThreads < n_list ? slist[tid + j * kThreads] : ~0u;
+        __syncthreads();   // the list area is reused below
+        if (K <= lds_cap)
+            nms_ranked<NMS, N>(lds_area, ent, K, bitmap, R2, nw, y0, W, bprefix, rprefix, frame, lk, t);
+        else
+            nms_ranked<NMS, N>(reinterpret_cast<uint16_t*>(slot), ent, K, bitmap, R2, nw, y0, W,
+                               bprefix, rprefix, frame, lk, t);
     } else {
         for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {
             const uint32_t row = wi / nw;
@@ -967,6 +1002,7 @@ void fast_sweep_kernel(BandParams P) {
         } else {
             // more keypoints than the list holds: the band's slot is the scratch
             band_nms_spill<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap,
+                                   reinterpret_cast<uint16_t*>(smem_raw + L.pq), L.nms_area_entries,
                                    reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
                                    reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
                                    reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),

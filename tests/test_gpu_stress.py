@@ -88,3 +88,39 @@ def test_config4_exact_batch(s1_batch):
     max-t NMS -- launched twice (device-side equality), frame 0 and the 3 densest frames
     against the oracle."""
     launch_twice_and_check(s1_batch, 16, 9, 1, n_check=3)
+
+
+@pytest.mark.parametrize("nms", [1, 2])
+def test_nms_overflow_tiers(nms):
+    """Bands whose keypoints overflow the LDS score list, at every density the band NMS pass
+    distinguishes (band_nms_spill): ranked scores in LDS, ranked scores in the band's slot,
+    and no stored scores (recompute all).  Frames mix S1 rows with uniform-noise rows (~28%
+    keypoints at t=16 n=9) at rates from 3% to 60%, so band densities sweep across the tiers;
+    every frame is checked against the oracle."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    frames = []
+    for k, rate in enumerate((0.03, 0.06, 0.1, 0.15, 0.2, 0.3, 0.45, 0.6)):
+        f = workloads.s1_frame(400 + k)
+        noisy = rng.random(H) < rate
+        f[noisy] = rng.integers(0, 256, (int(noisy.sum()), W), dtype=np.uint8)
+        frames.append(f)
+    batch = torch.from_numpy(np.stack(frames)).cuda()
+    cfg = Config(16, 9, NonMaximalSuppression(nms))
+    F = batch.shape[0]
+    offs = torch.zeros(F + 1, dtype=torch.int64, device="cuda")
+    out = torch.empty((F * W * H // 4, 2), dtype=torch.int32, device="cuda")
+    ctx = fast_hip.context(0)
+    for geometry in (0, 1):                 # the batch's own geometry, then the tall bands
+        ctx.set_geometry(geometry)
+        try:
+            fast_hip.detect_device(batch, cfg, out, offs)
+            torch.cuda.synchronize()
+        finally:
+            ctx.set_geometry(0)
+        o = offs.cpu().numpy()
+        for f in range(F):
+            got = out[o[f]:o[f + 1]].cpu().numpy().astype(np.uint32)
+            want = oracle.detect(frames[f], 16, 9, nms)
+            assert np.array_equal(got, want), (geometry, f, nms, len(got), len(want))
