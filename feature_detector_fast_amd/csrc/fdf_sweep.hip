@@ -103,8 +103,10 @@ struct SweepShared {
     uint32_t* stage;       // 64 pixels of the batch being issued: (row - ys) << 10 | strip column
     uint32_t* bitmap;      // band keypoints: bitmap row i = image row yb + i, words_per_row each
     uint32_t* slist;       // NMS: the band's keypoints as (bitmap row * W + x) << 12 | score
-    uint32_t* slist_n;     // entries appended (past slist_cap only counted)
+    uint32_t* slist_n;     // entries appended (the list, then the spill, then only counted)
     uint32_t slist_cap;    // kScoreListCap, or 0 when a position does not fit 20 bits
+    uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
+    uint32_t spill_cap;    // slot words (0 with slist_cap 0)
 };
 
 struct UnitCtx {
@@ -294,9 +296,8 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
     const bool is_kp = b.act && (kb || kd);
     if (is_kp) atomicOr(&sh.bitmap[(y - u.yb) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
     if constexpr (NMS != kNmsOff) {
-        // scores go to the band's LDS list; past its capacity they are only counted (the
-        // band NMS pass then ranks the listed ones into the band's slot and recomputes the
-        // rest from the frame)
+        // scores go to the band's LDS list, past its capacity to the band's slot (global),
+        // past that they are only counted (the band NMS pass then recomputes all scores)
         const uint64_t bal = wave_ballot(is_kp);
         if (bal) {
             uint32_t base = 0;
@@ -313,8 +314,9 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
                     score = score_sum_abs_packed(c, w, u.t);
                 }
                 const uint32_t idx = base + lanes_below(bal);
-                if (idx < sh.slist_cap)
-                    sh.slist[idx] = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
+                const uint32_t e = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
+                if (idx < sh.slist_cap) sh.slist[idx] = e;
+                else if (idx - sh.slist_cap < sh.spill_cap) sh.spill[idx - sh.slist_cap] = e;
             }
         }
     }
@@ -621,12 +623,79 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
     return *total;
 }
 
-// Band NMS (src/fast_simd.rs:589-616) from the LDS score list, in place on the keypoint
+// Strict 3x3 maximum of list entry e (src/fast_simd.rs:596-615) against the scores of its
+// neighbouring keypoints, read by raster rank from `sranked`; rows 3 / h-4 and the rows
+// outside the band are reported as suppressed / not compared by the caller's rules below.
+// Returns e with its score field replaced by 1 (suppressed) or 0 (kept).
+__device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap, uint32_t nw,
+                                              uint32_t nb_blocks, uint32_t y0, uint32_t W,
+                                              uint32_t H, const uint16_t* sranked,
+                                              const uint16_t* bprefix, const uint32_t* rprefix) {
+    const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+    const uint32_t y = y0 - 1 + row;
+    const uint32_t own = e & 0xfffu;
+    bool suppressed = y == 3 || y == H - 4;
+    if (own != 0 && !suppressed) {
+        uint32_t mx = 0;
+        const uint32_t mid = bits3(bitmap + row * nw, (int)x);
+        if (mid & 5u) {
+            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+            if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
+            if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
+        }
+#pragma unroll
+        for (int d = -1; d <= 1; d += 2) {
+            const uint32_t nbits = bits3(bitmap + (row + d) * nw, (int)x);
+            if (nbits) {
+                uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    if ((nbits >> k) & 1u) {
+                        mx = max(mx, (uint32_t)sranked[r]);
+                        ++r;
+                    }
+                }
+            }
+        }
+        suppressed = own <= mx;
+    }
+    return (e & ~0xfffu) | (suppressed ? 1u : 0u);
+}
+
+// Rank-order scatter of list entry e: a keypoint with a neighbouring keypoint puts its score
+// at its raster rank; an isolated one is kept without comparison, marked by a zero score.
+__device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitmap, uint32_t nw,
+                                                uint32_t R2, uint32_t nb_blocks, uint32_t W,
+                                                uint16_t* sranked, const uint16_t* bprefix,
+                                                const uint32_t* rprefix) {
+    const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+    if (neighbour_bits(bitmap, nw, R2, row, x) == 0) return e & ~0xfffu;
+    sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
+    return e;
+}
+
+__device__ __forceinline__ void nms_clear(uint32_t e, uint32_t* bitmap, uint32_t nw, uint32_t W) {
+    if ((e & 0xfffu) == 1u) {
+        const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+        atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
+    }
+}
+
+__device__ __forceinline__ bool in_band_rows(uint32_t e, uint32_t W, uint32_t R2) {
+    const uint32_t row = (e >> 12) / W;
+    return row != 0 && row != R2 - 1;                 // bitmap rows 0, R2-1: neighbours only
+}
+
+// Band NMS (src/fast_simd.rs:589-616) from the band's score list, in place on the keypoint
 // bitmap (bitmap rows 0 and rows + 1 are the rows just outside the band, neighbours only).
 // The list holds every keypoint of the bitmap once; its scores are scattered into raster
 // rank order, then each keypoint of the band's own rows reads its neighbours' scores by
 // rank, and the suppressed ones are cleared once every comparison has read the bitmap.
 // Rows 3 and h-4 are never output (:590-592, :342).
+//   n <= cap: the list is in LDS and the ranked scores go to the FIFO area.
+//   n > cap (the band_nms_spill variant): entries past the LDS list were appended to the
+//   band's slot (`spill`); the LDS entries move to registers (kSpillPer per thread), so the
+//   ranked scores can use the whole FIFO + staging + list area.
 template <int NMS>
 __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
                              uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
@@ -635,54 +704,51 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
     const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
     band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
     if (flags & kFlagNmsPrefixOnly) return;
-    // scores of keypoints with a neighbouring keypoint into rank order (the others' scores are
-    // never read: an isolated keypoint is kept, and marked by a zero score field)
-    for (uint32_t i = tid; i < n; i += kThreads) {
-        const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
-        if (neighbour_bits(bitmap, nw, R2, row, x) == 0) slist[i] = e & ~0xfffu;
-        else sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += kThreads) {
-        const uint32_t e = slist[i], pos = e >> 12, row = pos / W, x = pos - row * W;
-        if (row == 0 || row == R2 - 1) continue;          // rows outside the band
-        const uint32_t y = y0 - 1 + row;
-        const uint32_t own = e & 0xfffu;
-        bool suppressed = y == 3 || y == H - 4;
-        if (own != 0 && !suppressed) {
-            uint32_t mx = 0;
-            const uint32_t mid = bits3(bitmap + row * nw, (int)x);
-            if (mid & 5u) {
-                const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
-                if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
-                if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
-            }
-#pragma unroll
-            for (int d = -1; d <= 1; d += 2) {
-                const uint32_t nbits = bits3(bitmap + (row + d) * nw, (int)x);
-                if (nbits) {
-                    uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        if ((nbits >> k) & 1u) {
-                            mx = max(mx, (uint32_t)sranked[r]);
-                            ++r;
-                        }
-                    }
-                }
-            }
-            suppressed = own <= mx;
-        }
-        slist[i] = (e & ~0xfffu) | (suppressed ? 1u : 0u);
-    }
+    for (uint32_t i = tid; i < n; i += kThreads)
+        slist[i] = nms_scatter(slist[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i];
-        if ((e & 0xfffu) == 1u) {
-            const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
-            atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
-        }
+        if (in_band_rows(e, W, R2))
+            slist[i] = nms_entry(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
     }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) nms_clear(slist[i], bitmap, nw, W);
+    __syncthreads();
+}
+
+constexpr uint32_t kSpillPer = kScoreListCap / kThreads;
+
+template <int NMS>
+__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                               uint32_t H, const uint32_t* slist, uint32_t cap, uint32_t* spill,
+                               uint32_t n, uint16_t* sranked, uint16_t* bprefix, uint32_t* rprefix,
+                               uint32_t* total) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    uint32_t ent[kSpillPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j) ent[j] = slist[tid + j * kThreads];
+    band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);   // barriers: list area free
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j)
+        ent[j] = nms_scatter(ent[j], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
+    for (uint32_t i = tid; i < n - cap; i += kThreads)
+        spill[i] = nms_scatter(spill[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j)
+        if (in_band_rows(ent[j], W, R2))
+            ent[j] = nms_entry(ent[j], bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+    for (uint32_t i = tid; i < n - cap; i += kThreads) {
+        const uint32_t e = spill[i];
+        if (in_band_rows(e, W, R2))
+            spill[i] = nms_entry(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j) nms_clear(ent[j], bitmap, nw, W);
+    for (uint32_t i = tid; i < n - cap; i += kThreads) nms_clear(spill[i], bitmap, nw, W);
     __syncthreads();
 }
 
@@ -707,167 +773,48 @@ __device__ __forceinline__ uint32_t keypoint_score(const __amdgpu_buffer_rsrc_t&
     }
 }
 
-// Band NMS over ranked scores `sr` (u16 per bitmap keypoint, raster rank order; LDS or the
-// band's slot), for a band whose score list overflowed.  `ent` holds this thread's share of
-// the list (kScoreListCap / kThreads entries, ~0 = none):
-//  1. every rank is set to kUnset and the listed scores are scattered to their ranks;
-//  2. keypoints that take part in a comparison (those with a neighbouring keypoint) and were
-//     not listed get their score recomputed from the frame;
-//  3. each keypoint of the band's rows compares its score with its neighbours', marking the
-//     suppressed ones in the score's top bit;
-//  4. one wave per bitmap row clears the marked keypoints (lane = word, ranks from a wave
-//     scan of the row's original words; a row's ranks only depend on that row and the row
-//     prefixes, so rows can change independently).
-constexpr uint32_t kSpillPer = kScoreListCap / kThreads;
-constexpr uint16_t kUnset = 0x7fffu, kMark = 0x8000u;
-
+// Band NMS for bands too dense for the list and its spill (more keypoints than the LDS
+// list plus the slot hold, or a frame too wide for 20-bit list positions): no scores are
+// stored.  Each keypoint with a neighbouring keypoint recomputes its own and its neighbours'
+// scores; the kill masks go to the slot (one word per bitmap word, exactly the slot's size)
+// and are applied after.  Rows 3 and h-4 are never output (:590-592, :342); the caller
+// clears them.
 template <int NMS, int N>
-__device__ __forceinline__ void nms_ranked(uint16_t* sr, const uint32_t (&ent)[kSpillPer],
-                                           uint32_t K, uint32_t* bitmap, uint32_t R2, uint32_t nw,
-                                           uint32_t y0, uint32_t W, const uint16_t* bprefix,
-                                           const uint32_t* rprefix,
-                                           const __amdgpu_buffer_rsrc_t& frame,
-                                           const LerpConsts& lk, uint32_t t) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
-    for (uint32_t i = tid; i < K; i += kThreads) sr[i] = kUnset;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kSpillPer; ++j) {
-        const uint32_t e = ent[j];
-        if (e == ~0u) continue;
-        const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
-        if (neighbour_bits(bitmap, nw, R2, row, x))
-            sr[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
-    }
-    __syncthreads();
-    for (uint32_t wi = tid; wi < R2 * nw; wi += kThreads) {   // unlisted: recompute
-        const uint32_t row = wi / nw;
-        uint32_t bits = bitmap[wi];
-        while (bits) {
-            const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
-            bits &= bits - 1;
-            if (!neighbour_bits(bitmap, nw, R2, row, x)) continue;
-            const uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
-            if (sr[r] == kUnset)
-                sr[r] = (uint16_t)keypoint_score<NMS, N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), lk, t);
-        }
-    }
-    __syncthreads();
-    for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {   // compare
-        const uint32_t row = wi / nw;
-        uint32_t bits = bitmap[wi];
-        while (bits) {
-            const uint32_t x = (wi - row * nw) * 32 + __builtin_ctz(bits);
-            bits &= bits - 1;
-            const uint32_t mid = bits3(bitmap + row * nw, (int)x);
-            const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
-            const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
-            if (((mid & 5u) | up | dn) == 0) continue;
-            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
-            const uint32_t own = sr[ro] & 0x7fffu;
-            uint32_t mx = 0;
-            if (mid & 1u) mx = max(mx, sr[ro - 1] & 0x7fffu);
-            if (mid & 4u) mx = max(mx, sr[ro + 1] & 0x7fffu);
-#pragma unroll
-            for (int d = -1; d <= 1; d += 2) {
-                const uint32_t nbits = d < 0 ? up : dn;
-                if (nbits) {
-                    uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        if ((nbits >> k) & 1u) {
-                            mx = max(mx, sr[r] & 0x7fffu);
-                            ++r;
-                        }
-                    }
-                }
-            }
-            if (own <= mx) sr[ro] = (uint16_t)(own | kMark);
-        }
-    }
-    __syncthreads();
-    for (uint32_t row = 1 + wave; row + 1 < R2; row += kWaves) {   // clear
-        uint32_t* rw = bitmap + row * nw;
-        uint32_t carry = rprefix[row];
-        for (uint32_t k0 = 0; k0 < nw; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            const uint32_t v = k < nw ? rw[k] : 0u;
-            const uint32_t c = __popc(v);
-            const uint32_t incl = wave_incl_scan(c);
-            uint32_t r = carry + incl - c, bits = v, kill = 0;
-            carry += __builtin_amdgcn_readlane(incl, 63);
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
-                if (sr[r] & kMark) kill |= 1u << bit;
-                ++r;
-            }
-            if (kill) rw[k] = v & ~kill;
-        }
-    }
-}
-
-// Band NMS when the band has more keypoints than the LDS score list holds (dense images):
-// with K keypoints in the band's bitmap, the ranked scores go to the LDS area the FIFOs,
-// staging and list occupied during the sweep (K <= lds_cap; the list is first moved to
-// registers), else to the band's output slot, which is scratch until the band writes its
-// result (2 K <= slot bytes), see nms_ranked.  A band denser still stores no scores: each
-// keypoint with a neighbouring keypoint recomputes its own and its neighbours' scores, the
-// kill masks go to the slot (one word per bitmap word, exactly the slot's size) and are
-// applied after.  Rows 3 and h-4 are never output (:590-592, :342); the caller clears them.
-template <int NMS, int N>
-__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
-                               uint32_t H, const uint32_t* slist, uint32_t n_list, uint16_t* lds_area,
-                               uint32_t lds_cap, uint16_t* bprefix, uint32_t* rprefix,
-                               uint32_t* total, uint32_t* slot, uint32_t slot_bytes,
-                               const __amdgpu_buffer_rsrc_t& frame, const LerpConsts& lk, uint32_t t) {
+__device__ void band_nms_dense(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0,
+                               uint32_t W, uint32_t* slot, const __amdgpu_buffer_rsrc_t& frame,
+                               const LerpConsts& lk, uint32_t t) {
     const uint32_t tid = threadIdx.x;
     const uint32_t R2 = rows + 2;
-    const uint32_t K = band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
-    if (K <= lds_cap || 2ull * K <= slot_bytes) {
-        uint32_t ent[kSpillPer];
+    for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {
+        const uint32_t row = wi / nw;
+        uint32_t bits = bitmap[wi], kill = 0;
+        while (bits) {
+            const uint32_t bit = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const uint32_t x = (wi - row * nw) * 32 + bit;
+            const int y = (int)(y0 - 1 + row);
+            const uint32_t mid = bits3(bitmap + row * nw, (int)x) & 5u;
+            const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
+            const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
+            if ((mid | up | dn) == 0) continue;
+            const uint32_t own = keypoint_score<NMS, N>(frame, (int)W, (int)x, y, lk, t);
+            bool suppressed = false;
 #pragma unroll
-        for (uint32_t j = 0; j < kSpillPer; ++j)
-            ent[j] = tid + j * kThreads < n_list ? slist[tid + j * kThreads] : ~0u;
-        __syncthreads();   // the list area is reused below
-        if (K <= lds_cap)
-            nms_ranked<NMS, N>(lds_area, ent, K, bitmap, R2, nw, y0, W, bprefix, rprefix, frame, lk, t);
-        else
-            nms_ranked<NMS, N>(reinterpret_cast<uint16_t*>(slot), ent, K, bitmap, R2, nw, y0, W,
-                               bprefix, rprefix, frame, lk, t);
-    } else {
-        for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {
-            const uint32_t row = wi / nw;
-            uint32_t bits = bitmap[wi], kill = 0;
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t x = (wi - row * nw) * 32 + bit;
-                const int y = (int)(y0 - 1 + row);
-                const uint32_t mid = bits3(bitmap + row * nw, (int)x) & 5u;
-                const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
-                const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
-                if ((mid | up | dn) == 0) continue;
-                const uint32_t own = keypoint_score<NMS, N>(frame, (int)W, (int)x, y, lk, t);
-                bool suppressed = false;
+            for (int d = -1; d <= 1; ++d) {
+                const uint32_t nbits = d < 0 ? up : (d == 0 ? mid : dn);
 #pragma unroll
-                for (int d = -1; d <= 1; ++d) {
-                    const uint32_t nbits = d < 0 ? up : (d == 0 ? mid : dn);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        if (!suppressed && ((nbits >> k) & 1u) &&
-                            keypoint_score<NMS, N>(frame, (int)W, (int)x - 1 + k, y + d, lk, t) >= own)
-                            suppressed = true;
-                    }
+                for (int k = 0; k < 3; ++k) {
+                    if (!suppressed && ((nbits >> k) & 1u) &&
+                        keypoint_score<NMS, N>(frame, (int)W, (int)x - 1 + k, y + d, lk, t) >= own)
+                        suppressed = true;
                 }
-                if (suppressed) kill |= 1u << bit;
             }
-            slot[wi - nw] = kill;
+            if (suppressed) kill |= 1u << bit;
         }
-        __syncthreads();
-        for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) bitmap[wi] &= ~slot[wi - nw];
+        slot[wi - nw] = kill;
     }
+    __syncthreads();
+    for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) bitmap[wi] &= ~slot[wi - nw];
     __syncthreads();
 }
 
@@ -937,6 +884,8 @@ void fast_sweep_kernel(BandParams P) {
     sh.slist_n = unit_ctr + 1;
     // list positions are (bitmap row * W + x) in 20 bits
     sh.slist_cap = (uint64_t)(rows + 2 * halo) * W <= (1u << 20) ? kScoreListCap : 0u;
+    sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
+    sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
@@ -999,14 +948,16 @@ void fast_sweep_kernel(BandParams P) {
                               reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
                               reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
                               ablation_flags(P.flags));
+        } else if (n - sh.slist_cap <= sh.spill_cap && n <= L.nms_area_entries) {
+            // more keypoints than the LDS list holds: the rest were appended to the slot
+            band_nms_spill<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap, sh.spill, n,
+                                reinterpret_cast<uint16_t*>(smem_raw + L.pq),
+                                reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                                reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2);
         } else {
-            // more keypoints than the list holds: the band's slot is the scratch
-            band_nms_spill<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap,
-                                   reinterpret_cast<uint16_t*>(smem_raw + L.pq), L.nms_area_entries,
-                                   reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                                   reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+            band_nms_dense<NMS, N>(bitmap, rows, nw, y0, W,
                                    reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
-                                   P.slot_bytes, rs_exact, lk, P.threshold);
+                                   rs_exact, lk, P.threshold);
             // rows 3 and h - 4 keep no keypoints (they were neighbours only)
             for (uint32_t y : {3u, H - 4u}) {
                 if (y < y0 || y >= y0 + rows) continue;

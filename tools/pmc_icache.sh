@@ -1,4 +1,6 @@
 #!/bin/bash
+# ablation switches live in the debug build only (make debug)
+export FDF_LIB_PATH=${FDF_LIB_PATH:-$(cd "$(dirname "$0")/.." && pwd)/build/libfdf_debug.so}
 # Instruction-issue and instruction-cache counters for ablation variants (one --pmc set per
 # rocprofv3 run).  Usage: tools/pmc_icache.sh OUTDIR VARIANT...
 O=$1; shift
@@ -16,7 +18,7 @@ for V in "$@"; do
     D="$O/${V//:/_}/p$i"
     mkdir -p "$D"
     timeout -k 10 120 rocprofv3 --pmc $set -d "$D" -o p --output-format csv -- \
-        python3 tools/ablate.py --rounds 1 --iters 1 --variants "$V" > "$D.log" 2>&1 || echo "pass $i failed for $V"
+        python3 tools/ablate.py --rounds 1 --iters 1 $ABL_ARGS --variants "$V" > "$D.log" 2>&1 || echo "pass $i failed for $V"
   done
   echo "== $V"
   python3 tools/pmc_summary.py "$O/${V//:/_}"/p*
