@@ -118,6 +118,7 @@ struct UnitCtx {
     uint32_t lane;
     uint32_t head, tail;   // candidate FIFO: entries [head, tail) at pq[i % kSweepPixelQ]
     int ys;                // first row the unit sweeps (FIFO rows are relative to it)
+    int rowbase;           // (ys - 3) * W: frame offset of the window row y - 3 for FIFO row 0
     uint32_t flags;        // BandParams::flags (ablation runs only)
 };
 
@@ -170,6 +171,20 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Position of the j-th (from 0) set bit of a 16-bit mask that has more than j set bits.
+__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t j) {
+    uint32_t bit = 0;
+#pragma unroll
+    for (uint32_t w = 8; w >= 1; w >>= 1) {
+        const uint32_t c = __popc(m & ((1u << w) - 1u));
+        const bool up = j >= c;
+        j -= up ? c : 0u;
+        m = up ? m >> w : m;
+        bit += up ? w : 0u;
+    }
+    return bit;
 }
 
 // Pops the next 64 candidate pixels (fewer only when `force`: a flush) and starts their
@@ -226,7 +241,7 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
                     ++pos;
                 }
             }
-#else
+#elif defined(FDF_EXPAND_LOOP)
             // this lane writes min(k, 64 - excl) pixels; a wave-uniform loop over the most
             // any lane writes (no per-iteration ballot)
             const uint32_t cnt = excl < 64u ? min(k, 64u - excl) : 0u;
@@ -238,6 +253,33 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
                     sh.stage[pos + it] = rl | ((bit & 3u) << 2) | (bit >> 2);
                 }
             }
+#else
+            // no per-pixel loop: entry lane e marks the slot its pixels start at, a wave
+            // prefix-max turns the marks into each batch lane's entry, and the lane selects
+            // its bit of that entry's mask (binary search over popcounts)
+            sh.stage[lane] = 0u;
+            if (has && k != 0u && excl < 64u) sh.stage[excl] = lane;
+            // other lanes' stores feed this load: without the (instruction-free) wavefront
+            // fence the compiler forwards the lane's own zero store (per-thread semantics)
+            // and loads only where it stored
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            uint32_t src = sh.stage[lane];
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x111, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x112, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x114, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x118, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x142, 0xa, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x143, 0xc, 0xf, false));
+            const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)e);
+            const uint32_t sx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)excl);
+            {
+                const uint32_t bit = select_bit(se & 0xffffu, lane - sx);
+                // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column
+                if (lane < min(total, 64u))
+                    sh.stage[lane] = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
+            }
+            // the partial entry keeps the bits past the ones taken
+            if (has && excl < 64u && inc > 64u) m &= ~0u << select_bit(m, 64u - excl);
 #endif
             // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
             const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
@@ -248,7 +290,8 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             if (b.act) {
                 const uint32_t sc = sh.stage[lane];
                 b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
-                o = ((int)(b.code >> 10) - 3) * W + u.S - LC + (int)(b.code & 1023u);
+                // rows relative to the unit (< 2^10) times W (< 2^16): a 24-bit multiply
+                o = u.rowbase + (int)__umul24(sc >> 10, (uint32_t)W) + u.S - LC + (int)(sc & 1023u);
             }
         }
     }
@@ -294,7 +337,7 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
     lane_segment_test_packed<N>(c, w, lk, kb, kd);
     // every queued pixel is a centre of the unit's strip and tested rows (vmask, p0 .. p1)
     const bool is_kp = b.act && (kb || kd);
-    if (is_kp) atomicOr(&sh.bitmap[(y - u.yb) * u.nw + ((uint32_t)x >> 5)], 1u << (x & 31));
+    if (is_kp) atomicOr(&sh.bitmap[__umul24((uint32_t)(y - u.yb), u.nw) + ((uint32_t)x >> 5)], 1u << (x & 31));
     if constexpr (NMS != kNmsOff) {
         // scores go to the band's LDS list, past its capacity to the band's slot (global),
         // past that they are only counted (the band NMS pass then recomputes all scores)
@@ -314,7 +357,7 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
                     score = score_sum_abs_packed(c, w, u.t);
                 }
                 const uint32_t idx = base + lanes_below(bal);
-                const uint32_t e = (((uint32_t)(y - u.yb) * u.src.W + (uint32_t)x) << 12) | score;
+                const uint32_t e = ((__umul24((uint32_t)(y - u.yb), u.src.W) + (uint32_t)x) << 12) | score;
                 if (idx < sh.slist_cap) sh.slist[idx] = e;
                 else if (idx - sh.slist_cap < sh.spill_cap) sh.spill[idx - sh.slist_cap] = e;
             }
@@ -394,6 +437,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     const int p0 = u.p0, p1 = u.p1;                    // rows run through the pre-filter
     const int ys = p0 - 3;                             // first row of vertical comparisons
     u.ys = ys;
+    u.rowbase = (ys - 3) * W;
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
     u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
     u.head = u.tail = 0;
