@@ -228,8 +228,11 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
         if (total >= 64u || (force && total != 0u)) {
             b.n = min(total, 64u);
             const uint32_t excl = inc - k;
-            uint32_t m = e & 0xffffu, pos = excl;
+            uint32_t m = e & 0xffffu;
+#if defined(FDF_BALLOT_EXPAND) || defined(FDF_EXPAND_LOOP)
+            uint32_t pos = excl;
             const uint32_t rl = (e >> 16) << 4;       // (row - ys) << 10 | lane << 4
+#endif
 #ifdef FDF_BALLOT_EXPAND
             for (;;) {
                 const bool wr = m != 0u && pos < 64u;
