@@ -40,6 +40,11 @@ struct fdf_ctx {
     uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
+    // compaction bases: two alternating buffers of per-group sums (kept zero between uses)
+    // and the fused-compaction ticket, all zeroed once at context creation
+    uint32_t* d_sums = nullptr;         // 2 x fdfk::kMaxGroupSums, then the ticket
+    int sums_parity = 0;
+    bool sums_dirty = false;            // a launch failed: re-zero before the next use
     // cross-stream ordering: the device work of the last enqueue (on any stream) completes
     // at `done`; the next enqueue on another stream waits for it first
     hipEvent_t done = nullptr;
@@ -205,6 +210,33 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     int rc;
     if ((rc = ensure(ctx, &ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), stream))) return rc;
     if ((rc = ensure(ctx, &ctx->d_counts, &ctx->counts_n, (size_t)ntasks, stream))) return rc;
+    if (!ctx->d_sums) {
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sums),
+                      (2 * fdfk::kMaxGroupSums + 4) * sizeof(uint32_t)) != hipSuccess) {
+            ctx->d_sums = nullptr;
+            return FDF_ERR_ALLOC;
+        }
+        ctx->sums_dirty = true;
+    }
+    if (ctx->sums_dirty) {
+        if (hipMemsetAsync(ctx->d_sums, 0, (2 * fdfk::kMaxGroupSums + 4) * sizeof(uint32_t),
+                           stream) != hipSuccess)
+            return FDF_ERR_DEVICE;
+        ctx->sums_dirty = false;
+    }
+    // fused compaction (the detector's last workgroup orders the bands) is built but off:
+    // every workgroup's device-scope release is an L2 writeback on gfx950 (buffer_wbl2 sc1),
+    // and one frame measured 87 us fused against 10 + 9 us as two launches
+#ifdef FDF_FUSED_COMPACT
+    const bool fused = ntasks <= fdfk::kFusedCompactTasks;
+#else
+    const bool fused = false;
+#endif
+    if (fused) tpg = (uint32_t)ntasks;                  // one group, run by the last band
+    const uint64_t ngroups = (ntasks + tpg - 1) / tpg;
+    const bool grouped = !fused && ngroups <= fdfk::kMaxGroupSums;
+    uint32_t* sums_now = ctx->d_sums + (size_t)ctx->sums_parity * fdfk::kMaxGroupSums;
+    uint32_t* sums_next = ctx->d_sums + (size_t)(1 - ctx->sums_parity) * fdfk::kMaxGroupSums;
     fdfk::BandParams p;
     p.frames = d_frames;
     p.frame_stride = frame_stride;
@@ -235,6 +267,13 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.out = d_out;
     c.cap = cap;
     c.frame_offsets = d_offsets;
+    c.group_sums = grouped ? sums_now : nullptr;
+    c.next_sums = sums_next;
+    p.group_sums = grouped ? sums_now : nullptr;
+    p.tasks_per_group = tpg;
+    p.ticket = ctx->d_sums + 2 * fdfk::kMaxGroupSums;
+    p.fused = fused ? 1u : 0u;
+    p.compact = c;
     hipEvent_t* ev = nullptr;
     if (ctx->timing && ctx->timed < kMaxTimedCalls) {
         while (ctx->ev.size() < 3 * (ctx->timed + 1)) {
@@ -245,9 +284,17 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         ev = &ctx->ev[3 * ctx->timed];
     }
     if (ev && hipEventRecord(ev[0], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    if (fdfk::launch_sweep(p, cfg->nms, cfg->count, stream) != hipSuccess) return FDF_ERR_DEVICE;
+    if (fdfk::launch_sweep(p, cfg->nms, cfg->count, stream) != hipSuccess) {
+        ctx->sums_dirty = true;
+        return FDF_ERR_DEVICE;
+    }
     if (ev && hipEventRecord(ev[1], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    if (fdfk::launch_compact(c, stream) != hipSuccess) return FDF_ERR_DEVICE;
+    // small grids compacted inside the detector launch (its last workgroup)
+    if (!fused && fdfk::launch_compact(c, stream) != hipSuccess) {
+        ctx->sums_dirty = true;
+        return FDF_ERR_DEVICE;
+    }
+    if (grouped) ctx->sums_parity ^= 1;
     if (ev) {
         if (hipEventRecord(ev[2], stream) != hipSuccess) return FDF_ERR_DEVICE;
         ++ctx->timed;
@@ -487,6 +534,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_scores);
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
+        (void)hipFree(ctx->d_sums);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         if (ctx->done) (void)hipEventDestroy(ctx->done);
         (void)hipStreamDestroy(ctx->stream);

@@ -124,6 +124,32 @@ __host__ __device__ inline uint32_t slot_bytes_for(uint32_t R, uint32_t nw) {
     return b < 256 ? 256 : b;
 }
 
+// Bands per compaction workgroup: enough groups (~1024) to spread the copy over the chip.
+__host__ __device__ inline uint32_t compact_tasks_per_group(uint32_t ntasks) {
+    const uint32_t t = ntasks / 1024;
+    return t < 1 ? 1u : (t > (uint32_t)kCompactTasks ? (uint32_t)kCompactTasks : t);
+}
+// Grids up to this many bands compact inside the detector launch: the last workgroup to
+// finish (a ticket) orders every band itself, so a single frame costs one launch.
+constexpr uint32_t kFusedCompactTasks = 256;
+
+// Per-group keypoint sums the detector accumulates (one atomic add per band) so that a
+// compaction group finds its output base by summing the groups before it, O(groups) instead
+// of O(tasks).  Two buffers alternate between launches: a launch reads one and its
+// compaction zeroes the other for the next launch.
+constexpr uint32_t kMaxGroupSums = 2048;
+struct CompactParams {
+    uint32_t width, height, rows, bands_per_frame, ntasks, words_per_row, slot_bytes;
+    uint32_t tasks_per_group;        // compact_tasks_per_group(ntasks)
+    const uint8_t* slots;
+    const uint32_t* counts;
+    uint2* out;
+    uint64_t cap;
+    uint64_t* frame_offsets;         // frames + 1 entries
+    const uint32_t* group_sums;      // per-group sums of this launch (NULL: sum the counts)
+    uint32_t* next_sums;             // zeroed here for the next launch (kMaxGroupSums entries)
+};
+
 struct BandParams {
     const uint8_t* frames;       // frame f at frames + f * frame_stride, rows packed (stride = width)
     uint64_t frame_stride;
@@ -138,22 +164,11 @@ struct BandParams {
     uint32_t* counts;            // ntasks keypoint counts (band order = raster order)
     uint32_t flags;              // kFlag* ablation switches, 0 in production
     uint32_t nstrips, nsub;      // sweep kernel: column strips x sub-bands per band
-};
-
-// Bands per compaction workgroup: enough groups (~1024) to spread the copy over the chip.
-__host__ __device__ inline uint32_t compact_tasks_per_group(uint32_t ntasks) {
-    const uint32_t t = ntasks / 1024;
-    return t < 1 ? 1u : (t > (uint32_t)kCompactTasks ? (uint32_t)kCompactTasks : t);
-}
-
-struct CompactParams {
-    uint32_t width, height, rows, bands_per_frame, ntasks, words_per_row, slot_bytes;
-    uint32_t tasks_per_group;        // compact_tasks_per_group(ntasks)
-    const uint8_t* slots;
-    const uint32_t* counts;
-    uint2* out;
-    uint64_t cap;
-    uint64_t* frame_offsets;         // frames + 1 entries
+    uint32_t* group_sums;        // += band count at [task / tasks_per_group] (NULL: none)
+    uint32_t tasks_per_group;
+    uint32_t* ticket;            // fused compaction: bands finished (the last one resets it)
+    uint32_t fused;              // 1: the last workgroup runs `compact` (ntasks <= kFusedCompactTasks)
+    CompactParams compact;
 };
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);

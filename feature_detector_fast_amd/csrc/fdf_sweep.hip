@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include "fdf_common.h"
+#include "fdf_compact.h"
 #include "fdf_kernels.h"
 
 namespace fdfk {
@@ -108,6 +109,10 @@ struct SweepShared {
     uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
 };
+
+// max-t list entries whose score is computed by the NMS pass: score field kScorePending |
+// polarity (1 = dark); real scores are <= 255
+constexpr uint32_t kScorePending = 0x800u;
 
 struct UnitCtx {
     RowSource src;
@@ -352,10 +357,19 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
             if (is_kp) {
                 uint32_t score;
                 if constexpr (NMS == kNmsMaxThreshold) {
+#ifndef FDF_DEFER_MAXT_SCORE
                     uint32_t p[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
                     score = score_max_threshold<N>(c, p, kd);
+#else
+                    // deferred (FDF_DEFER_MAXT_SCORE): only keypoints with a neighbouring
+                    // keypoint ever need their score (~28% of a batch's lanes are keypoints),
+                    // so the band NMS pass computes it then, one keypoint per lane
+                    // (nms_scatter).  Measured slower: 1080p max-t +0.9%, 4K max-t +6.6%
+                    // (the NMS pass waits on its gathers)
+                    score = kScorePending | (kd ? 1u : 0u);
+#endif
                 } else {
                     score = score_sum_abs_packed(c, w, u.t);
                 }
@@ -609,11 +623,14 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
                                        uint16_t* bprefix, uint32_t* rprefix, uint32_t* total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
-    if (nb_blocks <= 16) {
-        // one bitmap row per 16-lane DPP row: lane k counts block k, a row_shr scan turns the
-        // counts into the row's block prefixes and lane 15 ends with the row total
-        for (uint32_t base = 0; base < R2; base += kThreads / 16) {
-            const uint32_t row = base + tid / 16, k = tid & 15u;
+    if (nb_blocks <= 32) {
+        // one bitmap row per 16-lane DPP row (or per 32-lane half-wave when it has more than
+        // 16 blocks, e.g. 4K): lane k counts block k, a row_shr scan (+ row_bcast:15 across
+        // the two rows of a half) turns the counts into the row's block prefixes, and the
+        // row's last lane ends with the row total
+        const uint32_t span = nb_blocks <= 16 ? 16u : 32u;
+        for (uint32_t base = 0; base < R2; base += kThreads / span) {
+            const uint32_t row = base + tid / span, k = tid & (span - 1u);
             const bool act = row < R2 && k < nb_blocks;
             uint32_t cnt = 0;
             if (act) {
@@ -627,8 +644,10 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
             inc += __builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xf, 0xf, false);   // row_shr:2
             inc += __builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xf, 0xf, false);   // row_shr:4
             inc += __builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xf, 0xf, false);   // row_shr:8
+            if (span == 32u)
+                inc += __builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xa, 0xf, false);   // row_bcast:15
             if (act) bprefix[row * nb_blocks + k] = (uint16_t)(inc - cnt);
-            if (row < R2 && k == 15u) rprefix[row] = inc;
+            if (row < R2 && k == span - 1u) rprefix[row] = inc;
         }
     } else {
         for (uint32_t i = tid; i < R2 * nb_blocks; i += kThreads) {
@@ -709,14 +728,36 @@ __device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap
     return (e & ~0xfffu) | (suppressed ? 1u : 0u);
 }
 
+// Max-threshold score of the keypoint at (x, y) of known polarity, from the frame (the
+// sweep's windows and packing; deferred scores, see evaluate_batch).
+template <int N>
+__device__ __forceinline__ uint32_t keypoint_score_maxt(const __amdgpu_buffer_rsrc_t& rs, int W,
+                                                        int x, int y, bool dark) {
+    Batch b;
+    load_ring_windows(b, rs, (y - 3) * W + x, W);
+    uint32_t w[4], c;
+    pack_ring(b, w, c);
+    uint32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+    return score_max_threshold<N>(c, p, dark);
+}
+
 // Rank-order scatter of list entry e: a keypoint with a neighbouring keypoint puts its score
-// at its raster rank; an isolated one is kept without comparison, marked by a zero score.
+// at its raster rank (computing it first when it was deferred); an isolated one is kept
+// without comparison, marked by a zero score.
+template <int NMS, int N>
 __device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitmap, uint32_t nw,
                                                 uint32_t R2, uint32_t nb_blocks, uint32_t W,
-                                                uint16_t* sranked, const uint16_t* bprefix,
-                                                const uint32_t* rprefix) {
+                                                uint32_t y0, uint16_t* sranked,
+                                                const uint16_t* bprefix, const uint32_t* rprefix,
+                                                const __amdgpu_buffer_rsrc_t& frame) {
     const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
     if (neighbour_bits(bitmap, nw, R2, row, x) == 0) return e & ~0xfffu;
+    if constexpr (NMS == kNmsMaxThreshold) {
+        if (e & kScorePending)
+            e = (e & ~0xfffu) | keypoint_score_maxt<N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), e & 1u);
+    }
     sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
     return e;
 }
@@ -743,16 +784,18 @@ __device__ __forceinline__ bool in_band_rows(uint32_t e, uint32_t W, uint32_t R2
 //   n > cap (the band_nms_spill variant): entries past the LDS list were appended to the
 //   band's slot (`spill`); the LDS entries move to registers (kSpillPer per thread), so the
 //   ranked scores can use the whole FIFO + staging + list area.
-template <int NMS>
+template <int NMS, int N>
 __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
                              uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
-                             uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags) {
+                             uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags,
+                             __amdgpu_buffer_rsrc_t frame) {
     const uint32_t tid = threadIdx.x;
     const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
     band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
     if (flags & kFlagNmsPrefixOnly) return;
     for (uint32_t i = tid; i < n; i += kThreads)
-        slist[i] = nms_scatter(slist[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
+        slist[i] = nms_scatter<NMS, N>(slist[i], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
+                                       rprefix, frame);
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i];
@@ -766,11 +809,11 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
 
 constexpr uint32_t kSpillPer = kScoreListCap / kThreads;
 
-template <int NMS>
+template <int NMS, int N>
 __device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
                                uint32_t H, const uint32_t* slist, uint32_t cap, uint32_t* spill,
                                uint32_t n, uint16_t* sranked, uint16_t* bprefix, uint32_t* rprefix,
-                               uint32_t* total) {
+                               uint32_t* total, __amdgpu_buffer_rsrc_t frame) {
     const uint32_t tid = threadIdx.x;
     const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
     uint32_t ent[kSpillPer];
@@ -779,9 +822,11 @@ __device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
     band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);   // barriers: list area free
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j)
-        ent[j] = nms_scatter(ent[j], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
+        ent[j] = nms_scatter<NMS, N>(ent[j], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
+                                     rprefix, frame);
     for (uint32_t i = tid; i < n - cap; i += kThreads)
-        spill[i] = nms_scatter(spill[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
+        spill[i] = nms_scatter<NMS, N>(spill[i], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
+                                       rprefix, frame);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j)
@@ -828,8 +873,8 @@ __device__ __forceinline__ uint32_t keypoint_score(const __amdgpu_buffer_rsrc_t&
 // clears them.
 template <int NMS, int N>
 __device__ void band_nms_dense(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0,
-                               uint32_t W, uint32_t* slot, const __amdgpu_buffer_rsrc_t& frame,
-                               const LerpConsts& lk, uint32_t t) {
+                               uint32_t W, uint32_t* slot, __amdgpu_buffer_rsrc_t frame,
+                               LerpConsts lk, uint32_t t) {
     const uint32_t tid = threadIdx.x;
     const uint32_t R2 = rows + 2;
     for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {
@@ -865,25 +910,12 @@ __device__ void band_nms_dense(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
     __syncthreads();
 }
 
-// Occupancy target: kSweepWavesPerEU waves per SIMD (4: 128 VGPRs each, 2: 256).
-template <int NMS, int N>
-__global__ __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(kSweepWavesPerEU, kSweepWavesPerEU)))
-void fast_sweep_kernel(BandParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    constexpr int LC = kLaneCols;
-    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, NMS);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t lane = tid & 63;
-    const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
-    constexpr uint32_t halo = NMS == kNmsOff ? 0u : 1u;
-
-    // XCD-aware static task mapping: each XCD takes a contiguous range of bands (raster
+// The band (task) a workgroup sweeps.  XCD-aware static task mapping: each XCD takes a contiguous range of bands (raster
     // order), so consecutive bands of a frame land on one XCD (its L2 then serves the halo
     // rows two neighbouring bands share).  Within its range an XCD dispatches the frames'
     // full bands first and their (shorter) last bands at the end, where they fill the grid's
     // tail.
+__device__ __forceinline__ uint32_t band_task(const BandParams& P) {
     const uint32_t b = blockIdx.x;
     const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
     const uint32_t c0 = k8 * q8 + min(k8, r8), j = b >> 3;
@@ -904,6 +936,19 @@ void fast_sweep_kernel(BandParams P) {
         }
     }
 #endif
+    return task;
+}
+
+// Sweeps band `task`, runs its NMS and writes its slot; returns the band's keypoint count.
+template <int NMS, int N>
+__device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* smem_raw, uint32_t task) {
+    constexpr int LC = kLaneCols;
+    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, NMS);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63;
+    const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
+    constexpr uint32_t halo = NMS == kNmsOff ? 0u : 1u;
     const uint32_t frame = task / P.bands_per_frame;
     const uint32_t band = task - frame * P.bands_per_frame;
     const uint32_t y0 = 3 + band * P.rows;
@@ -911,10 +956,7 @@ void fast_sweep_kernel(BandParams P) {
 
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap);
     uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.misc);
-    if (P.threshold >= 255) {                                        // no pixel can pass
-        if (tid == 0) P.counts[task] = 0;
-        return;
-    }
+    if (P.threshold >= 255) return 0;                                // no pixel can pass
     uint32_t* unit_ctr = wave_sum + kWaves;
     for (uint32_t i = tid; i <= (rows + 2 * halo) * nw; i += kThreads) bitmap[i] = 0;   // + pad
     if (tid == 0) {
@@ -990,17 +1032,18 @@ void fast_sweep_kernel(BandParams P) {
         const uint32_t n = *sh.slist_n;
         if (ablation_flags(P.flags) & kFlagNoNms) {
         } else if (n <= sh.slist_cap) {
-            band_nms_lds<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, n,
-                              reinterpret_cast<uint16_t*>(smem_raw + L.pq),
-                              reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                              reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
-                              ablation_flags(P.flags));
+            band_nms_lds<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, n,
+                                 reinterpret_cast<uint16_t*>(smem_raw + L.pq),
+                                 reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                                 reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+                                 ablation_flags(P.flags), rs_exact);
         } else if (n - sh.slist_cap <= sh.spill_cap && n <= L.nms_area_entries) {
             // more keypoints than the LDS list holds: the rest were appended to the slot
-            band_nms_spill<NMS>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap, sh.spill, n,
-                                reinterpret_cast<uint16_t*>(smem_raw + L.pq),
-                                reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                                reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2);
+            band_nms_spill<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap, sh.spill, n,
+                                   reinterpret_cast<uint16_t*>(smem_raw + L.pq),
+                                   reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                                   reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+                                   rs_exact);
         } else {
             band_nms_dense<NMS, N>(bitmap, rows, nw, y0, W,
                                    reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
@@ -1037,8 +1080,7 @@ void fast_sweep_kernel(BandParams P) {
         before += (uint32_t)w < wave ? v : 0u;
         total += v;
     }
-    if (tid == 0) P.counts[task] = total;
-    if (ablation_flags(P.flags) & kFlagNoEmit) return;
+    if (ablation_flags(P.flags) & kFlagNoEmit) return total;
     uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
     if (total <= P.slot_bytes / 8) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
@@ -1075,8 +1117,7 @@ void fast_sweep_kernel(BandParams P) {
         before += (uint32_t)w < wave ? v : 0u;
         total += v;
     }
-    if (tid == 0) P.counts[task] = total;
-    if (ablation_flags(P.flags) & kFlagNoEmit) return;
+    if (ablation_flags(P.flags) & kFlagNoEmit) return total;
     uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
     if (total <= P.slot_bytes / 8) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
@@ -1099,6 +1140,44 @@ void fast_sweep_kernel(BandParams P) {
     } else {
         uint32_t* words = reinterpret_cast<uint32_t*>(slot);
         for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
+    }
+#endif
+    return total;
+}
+
+// Occupancy target: kSweepWavesPerEU waves per SIMD (4: 128 VGPRs each, 2: 256).
+template <int NMS, int N>
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(kSweepWavesPerEU, kSweepWavesPerEU)))
+void fast_sweep_kernel(BandParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    const uint32_t task = band_task(P);
+    const uint32_t total = sweep_band<NMS, N>(P, smem_raw, task);
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        P.counts[task] = total;
+        if (P.group_sums) atomicAdd(&P.group_sums[task / P.tasks_per_group], total);
+    }
+#ifdef FDF_FUSED_COMPACT
+    if (P.fused) {
+        // fused compaction (small grids): every band publishes its slot and count, and the
+        // last one to finish (a ticket) orders them all
+        __threadfence();
+        __syncthreads();
+        uint32_t* last = reinterpret_cast<uint32_t*>(smem_raw);
+        if (tid == 0) *last = atomicAdd(P.ticket, 1u) == P.ntasks - 1u ? 1u : 0u;
+        __syncthreads();
+        if (*last) {
+            __threadfence();
+            __syncthreads();
+            CompactShared& sm = *reinterpret_cast<CompactShared*>(smem_raw + 16);
+            const uint32_t ngroups = (P.ntasks + P.compact.tasks_per_group - 1) / P.compact.tasks_per_group;
+            for (uint32_t g = 0; g < ngroups; ++g) {
+                compact_group(P.compact, g, sm);
+                __syncthreads();
+            }
+            if (tid == 0) *P.ticket = 0u;           // for the next launch
+        }
     }
 #endif
 }
