@@ -552,6 +552,7 @@ def main(argv=None):
                        "frames_per_gpu": count, "width": W, "height": H,
                        "threshold": args.threshold, "count": args.count, "nms": args.nms,
                        "hbm_copies": len(copies),
+                       "workspace_bytes": ctx.workspace_bytes(),
                        "parallelism": f"frame-sharded x{world} (no collective)"},
             "keypoints_per_step": int(kp_total),
             "roofline": roofline,

@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "fdf_detect_batch_scored", "fdf_score_device", "fdf_pipeline_create",
     "fdf_pipeline_destroy", "fdf_pipeline_acquire", "fdf_pipeline_submit", "fdf_pipeline_push",
     "fdf_pipeline_collect", "fdf_ctx_set_geometry", "fdf_ctx_timing_samples", "fdf_fetch_last",
-    "fdf_detect_batch_multi", "fdf_fetch_last_multi",
+    "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
 )
 
 
@@ -144,6 +144,8 @@ def load():
     lib.fdf_pipeline_push.argtypes = [vp, vp, u32, sz, ctypes.POINTER(u64)]
     lib.fdf_pipeline_collect.restype = ctypes.c_int
     lib.fdf_pipeline_collect.argtypes = [vp, u64, vp, vp, sz, vp, ctypes.POINTER(sz)]
+    lib.fdf_ctx_workspace_bytes.restype = ctypes.c_int
+    lib.fdf_ctx_workspace_bytes.argtypes = [vp, ctypes.POINTER(u64)]
     lib.fdf_ctx_set_geometry.restype = ctypes.c_int
     lib.fdf_ctx_set_geometry.argtypes = [vp, u32]
     lib.fdf_ctx_timing_samples.restype = ctypes.c_int
@@ -207,6 +209,12 @@ class Context:
             check(self._lib.fdf_ctx_timing_samples(self.handle, det.ctypes.data, com.ctypes.data,
                                                    n.value, ctypes.byref(n)))
         return det, com
+
+    def workspace_bytes(self):
+        """Device bytes held by the context's workspace (fdf_ctx_workspace_bytes)."""
+        v = ctypes.c_uint64()
+        check(self._lib.fdf_ctx_workspace_bytes(self.handle, ctypes.byref(v)))
+        return v.value
 
     def set_geometry(self, min_tasks=0):
         """Band geometry override (fdf_ctx_set_geometry): min_tasks=1 gives small jobs the

@@ -552,6 +552,16 @@ int fdf_ctx_set_timing(fdf_ctx* ctx, int enable) {
     return FDF_OK;
 }
 
+int fdf_ctx_workspace_bytes(fdf_ctx* ctx, uint64_t* bytes) {
+    if (!ctx || !bytes) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    *bytes = ctx->in_bytes + ctx->rgb_bytes + ctx->out_points * sizeof(uint2) +
+             ctx->offsets_n * sizeof(uint64_t) + ctx->scores_n * sizeof(uint16_t) +
+             ctx->slots_bytes + ctx->counts_n * sizeof(uint32_t) +
+             (ctx->d_sums ? (2 * fdfk::kMaxGroupSums + 4) * sizeof(uint32_t) : 0);
+    return FDF_OK;
+}
+
 int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
     if (!ctx) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);

@@ -104,6 +104,11 @@ int fdf_ctx_timing_samples(fdf_ctx* ctx, float* detect_ms, float* compact_ms, ui
  * large batches -- the parity tests reach those code paths with small inputs this way. */
 int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
 
+/* Device bytes the context's workspace holds now (host-API staging and output, per-band
+ * slots and counts, compaction sums).  Slots take 1/8 byte per pixel of the largest batch
+ * seen; nothing in the workspace scales with more than that. */
+int fdf_ctx_workspace_bytes(fdf_ctx* ctx, uint64_t* bytes);
+
 /*
  * Replaces fast_simd::detector(img, config) -> Vec<Point> (src/fast_simd.rs:847).
  * Host image (row-major u8, `stride_bytes` >= width; GrayImage always has stride == width),
