@@ -8,7 +8,7 @@ TAG=$1; shift
 O=gpurun_out/prof_$TAG
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-ARGS="--steps 10 --warmup 3 --cpu-seconds 0 --no-extras $*"
+ARGS="--cpu-seconds 0 --no-extras $*"   # the bench defaults (50 timed steps after 10 warm-up)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats" -o p -- \
     python3 bench.py $ARGS > "$O/bench_under_trace.json" 2> "$O/stats.log"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o p -- \
