@@ -15,10 +15,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude $(EXTRA_
 
 all: $(LIBFDF) oracle/liboracle.so oracle/libfast_avx2.so tests/cpp/test_cpp_api
 
-$(CSRC)/fdf_kernels.o: $(CSRC)/fdf_kernels.hip $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
+$(CSRC)/fdf_kernels.o: $(CSRC)/fdf_kernels.hip $(CSRC)/fdf_compact.h $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(CSRC)/fdf_sweep.o: $(CSRC)/fdf_sweep.hip $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
+$(CSRC)/fdf_sweep.o: $(CSRC)/fdf_sweep.hip $(CSRC)/fdf_sweep_impl.h $(CSRC)/fdf_compact.h $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/fdf_sweep_rgb.o: $(CSRC)/fdf_sweep_rgb.hip $(CSRC)/fdf_sweep_impl.h $(CSRC)/fdf_compact.h $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/fdf_api.o: $(CSRC)/fdf_api.cpp $(CSRC)/fdf_kernels.h include/fdf.h
@@ -27,7 +30,7 @@ $(CSRC)/fdf_api.o: $(CSRC)/fdf_api.cpp $(CSRC)/fdf_kernels.h include/fdf.h
 $(CSRC)/fdf_pipeline.o: $(CSRC)/fdf_pipeline.cpp include/fdf.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_api.o $(CSRC)/fdf_pipeline.o
+$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_sweep_rgb.o $(CSRC)/fdf_api.o $(CSRC)/fdf_pipeline.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle/liboracle.so: oracle/fast_oracle.c oracle/fast_oracle.h

@@ -324,6 +324,19 @@ def rgb_path(fast_hip, cfg, frames, out, offs, stream, nframes=256, steps=10):
     fast_hip.detect_device(grey_in, cfg, out, offs, stream=stream)
     torch.cuda.synchronize()
     n_grey = int(offs[F].item())
+    grey_same = n_rgb == n_grey and bool(torch.equal(pts_rgb, out[:n_grey]))
+    # the fused path: luma converted in the detector's loads (fdf_detect_device_rgb)
+    offs_f = torch.zeros(F + 1, dtype=torch.int64, device=frames.device)
+    for _ in range(3):
+        fast_hip.detect_device_rgb(rgb, cfg, out, offs_f, stream=stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fast_hip.detect_device_rgb(rgb, cfg, out, offs_f, stream=stream)
+    torch.cuda.synchronize()
+    elapsed_f = time.perf_counter() - t0
+    n_f = int(offs_f[-1].item())
+    fused_same = n_f == n_rgb and bool(torch.equal(out[:n_f], pts_rgb))
     gbps = 4.0 * F * H * W / (luma_ms * 1e-3) / 1e9
     res = {"workload": f"batch of {F} {W}x{H} RGB8 frames (grey repeated per channel)",
            "Mpix_s": round(F * H * W * steps / elapsed / 1e6, 1),
@@ -333,7 +346,10 @@ def rgb_path(fast_hip, cfg, frames, out, offs, stream, nframes=256, steps=10):
            "luma_roofline_frac": round(gbps / HBM_PEAK_GBS, 4),
            "luma_equals_grey": same,
            "keypoints_per_step": n_rgb,
-           "keypoints_equal_grey_path": n_rgb == n_grey and bool(torch.equal(pts_rgb, out[:n_grey]))}
+           "keypoints_equal_grey_path": grey_same,
+           "fused_Mpix_s": round(F * H * W * steps / elapsed_f / 1e6, 1),
+           "fused_ms_per_step": round(elapsed_f * 1e3 / steps, 4),
+           "fused_keypoints_equal_two_pass": fused_same}
     del rgb, grey, pts_rgb
     return res
 

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "fdf_pipeline_destroy", "fdf_pipeline_acquire", "fdf_pipeline_submit", "fdf_pipeline_push",
     "fdf_pipeline_collect", "fdf_ctx_set_geometry", "fdf_ctx_timing_samples", "fdf_fetch_last",
     "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
+    "fdf_detect_device_rgb",
 )
 
 
@@ -122,6 +123,8 @@ def load():
                                      ctypes.POINTER(sz)]
     lib.fdf_detect_device.restype = ctypes.c_int
     lib.fdf_detect_device.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp]
+    lib.fdf_detect_device_rgb.restype = ctypes.c_int
+    lib.fdf_detect_device_rgb.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp]
     lib.fdf_score_points.restype = ctypes.c_int
     lib.fdf_score_points.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, vp]
     lib.fdf_detect_scored.restype = ctypes.c_int

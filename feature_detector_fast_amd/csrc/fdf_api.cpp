@@ -26,6 +26,7 @@ struct LastResult {
     uint64_t total = 0;
     uint32_t n_frames = 0, width = 0, height = 0;
     fdf_config cfg{};
+    bool rgb = false;              // frames in d_rgb (RGB8); scores need their luma in d_in
 };
 
 struct fdf_ctx {
@@ -181,7 +182,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
 // workspace is shared).
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
-            uint64_t* d_offsets, hipStream_t stream) {
+            uint64_t* d_offsets, hipStream_t stream, bool rgb = false) {
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms,
                                        ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks);
     const uint32_t R = geo.R;
@@ -284,7 +285,8 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         ev = &ctx->ev[3 * ctx->timed];
     }
     if (ev && hipEventRecord(ev[0], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    if (fdfk::launch_sweep(p, cfg->nms, cfg->count, stream) != hipSuccess) {
+    if ((rgb ? fdfk::launch_sweep_rgb(p, cfg->nms, cfg->count, stream)
+             : fdfk::launch_sweep(p, cfg->nms, cfg->count, stream)) != hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
@@ -367,6 +369,10 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                                               hipMemcpyHostToDevice, ctx->stream);
         if (e != hipSuccess) return FDF_ERR_DEVICE;
     }
+    // RGB: a luma pass, then the grey detector.  The detector with luma converted in its
+    // loads (fdf_detect_device_rgb) is correct but measured 1.6x slower on 256 1080p frames:
+    // its 48-byte row loads need 12 registers each until converted, which spills and
+    // exposes the row latency
     if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
@@ -395,6 +401,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     ctx->last.width = w;
     ctx->last.height = h;
     ctx->last.cfg = *cfg;
+    ctx->last.rgb = false;          // the luma frames are in d_in
     return FDF_OK;
 }
 
@@ -407,6 +414,13 @@ int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
     if (out_scores) {
         int rc = ensure(ctx, &ctx->d_scores, &ctx->scores_n, n, ctx->stream);
         if (rc) return rc;
+        if (L.rgb) {   // the scores are computed from the luma frames
+            const size_t fb = (size_t)L.width * L.height;
+            if ((rc = ensure(ctx, &ctx->d_in, &ctx->in_bytes, fb * L.n_frames, ctx->stream))) return rc;
+            if (fdfk::launch_rgb_to_luma(ctx->d_rgb, L.n_frames, (uint32_t)fb, 3 * fb, ctx->d_in,
+                                         ctx->stream) != hipSuccess)
+                return FDF_ERR_DEVICE;
+        }
         e = fdfk::launch_score_frames(ctx->d_in, L.width, (uint64_t)L.width * L.height,
                                       L.n_frames, ctx->d_out, ctx->d_offsets, n,
                                       score_blocks(n, L.n_frames), score_kind(L.cfg.nms),
@@ -716,6 +730,34 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
     return enqueue(ctx, d_frames, n_frames, width, height,
                    n_frames > 1 ? frame_stride_bytes : (uint64_t)width * height, cfg,
                    reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s);
+}
+
+int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
+                          uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
+                          const fdf_config* cfg, fdf_point* d_out, uint64_t cap,
+                          uint64_t* d_frame_offsets, void* stream) {
+    if (!ctx || !d_frame_offsets) return FDF_ERR_ARG;
+    int rc = check_config(cfg);
+    if (rc) return rc;
+    int empty = 0;
+    rc = check_shape(width, height, &empty);
+    if (rc) return rc;
+    if (n_frames == 0) empty = 1;
+    if (!empty && (!d_frames || (cap && !d_out))) return FDF_ERR_ARG;
+    const uint64_t fb = 3ull * width * height;
+    if (fb > 0x7fffffffull) return FDF_ERR_SIZE;
+    if (n_frames > 1 && frame_stride_bytes < fb) return FDF_ERR_ARG;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    if (empty) {
+        return hipMemsetAsync(d_frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull), s) ==
+                       hipSuccess
+                   ? FDF_OK
+                   : FDF_ERR_DEVICE;
+    }
+    return enqueue(ctx, d_frames, n_frames, width, height, n_frames > 1 ? frame_stride_bytes : fb,
+                   cfg, reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s, true);
 }
 
 int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t height,

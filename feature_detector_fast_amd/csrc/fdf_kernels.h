@@ -173,6 +173,8 @@ struct BandParams {
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);
 hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
+// RGB8 frames (3 bytes per pixel, frame_stride in bytes), luma converted on load
+hipError_t launch_sweep_rgb(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
 hipError_t launch_rgb_to_luma(const uint8_t* rgb, uint32_t n_frames, uint32_t pixels,
                               uint64_t rgb_frame_stride, uint8_t* grey, hipStream_t stream);
 hipError_t launch_score_points(const uint8_t* img, uint32_t width, const uint2* pts,

@@ -1,0 +1,1307 @@
+// fdf_sweep_impl.h -- column-sweep FAST-9..16 kernel for MI355X (gfx950), the production path.
+// Included by fdf_sweep.hip (grey frames: FDF_SWEEP_RGB 0, namespace fdfk::grey) and
+// fdf_sweep_rgb.hip (RGB8 frames converted to luma in the row and window loads:
+// FDF_SWEEP_RGB 1, namespace fdfk::rgb); each translation unit instantiates its 24 kernels.
+//
+// Replaces detect<NONMAX>() (iwanders/feature_detector_fast src/fast_simd.rs:301-620) with
+// determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
+//
+// One workgroup (4 waves) owns a band of R full-width centre rows of one frame.  The band is
+// cut into units = (column strip) x (sub-band of rows); waves take units from an LDS counter
+// and sweep them top to bottom:
+//   * lane l owns 16 columns (one 16-byte buffer load per row); lanes 0 and 63 are halo
+//     lanes that only feed their neighbours, so a strip covers 62 x 16 centres;
+//   * pixel rows stream through a register ring of kSweepRing slots: kSweepRing - 4 row loads
+//     are in flight, none is guarded by a branch and none is copied, so the compiler's vmcnt
+//     bookkeeping keeps them in flight;
+//   * every pairwise comparison is made once and used by both of its pixels: the vertical
+//     pair (I(y), I(y+3)) gives S-flags for row y and N-flags for row y+3, the horizontal
+//     pair (I(x), I(x+3)) gives E-flags for x and W-flags for x+3 (a 3-byte shift, with the
+//     neighbouring lane's bytes via DPP).  Comparisons are byte-SWAR v_lerp_u8 (exact per
+//     byte, see fdf_common.h), so the cardinal pre-filter (src/fast_simd.rs:441-509) costs
+//     2 lerps per pixel;
+//   * candidate pixels go into a per-wave FIFO in LDS (one per lane per round).  Every
+//     kSweepIssue rows, once 64 are queued, a batch is issued: each lane gathers its pixel's
+//     7x7 neighbourhood with 7 row-window loads straight from the frame (the rows were just
+//     streamed, so these hit L2).  The batch is evaluated kSweepIssue rows later -- by then
+//     the row loads issued before it are due anyway, so waiting for it never drains the row
+//     prefetch -- with the per-lane VALU segment test (fdf_common.h).  Keypoints set their
+//     bit in the band's LDS bitmap; with NMS their score goes to the frame's score map.
+// NMS (src/fast_simd.rs:589-616) runs once the whole band is tested: the band also tests one
+// row above and below it, so every neighbour of its keypoints is in the bitmap, and each
+// keypoint is compared with the scores of the neighbours the bitmap marks.  The band's
+// keep-bits are then written to its output slot (its points in raster order, or the bitmap
+// if they do not fit) and compact_kernel orders all slots.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "fdf_common.h"
+#include "fdf_compact.h"
+#include "fdf_kernels.h"
+
+#ifndef FDF_SWEEP_NS
+#error "define FDF_SWEEP_RGB and FDF_SWEEP_NS before including fdf_sweep_impl.h"
+#endif
+
+namespace fdfk {
+namespace FDF_SWEEP_NS {
+
+// RGB8 input: 3 bytes per pixel, converted to luma as image 0.24.6 to_luma8 on load
+constexpr bool kRgb = FDF_SWEEP_RGB != 0;
+constexpr int kPx = kRgb ? 3 : 1;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+
+// A lane's LC bytes of one pixel row (LC / 4 dwords).
+template <int LC> struct LaneRow;
+template <> struct LaneRow<16> { using type = u32x4; };
+template <> struct LaneRow<8> { using type = u32x2; };
+
+// DPP whole-wave shifts (GFX9 encodings): lane i reads lane i+1 / lane i-1; the lane that
+// falls off the wave reads 0 (it is a halo lane whose results are never used).
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, false);   // wave_shl:1
+}
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+}
+
+struct RowSource {
+    __amdgpu_buffer_rsrc_t rs;   // the frame; num_records = W * H + 15, or W * H when EXACT
+    uint32_t W, H;
+    int ylast;                   // last row the unit needs: later prefetches read nothing
+    int tail_row;                // EXACT: rows >= tail_row may have windows crossing W * H
+};
+
+// Bytes [xb, xb+LC) of image row y: one LC-byte buffer load at any byte offset (gfx950
+// buffer loads need no alignment).  No branch, so the row prefetch stays a plain stream the
+// compiler's vmcnt bookkeeping can count.  Rows outside the frame and negative offsets read
+// 0; columns outside [0, W) hold neighbouring bytes (the next row, or up to 15 bytes past
+// the frame, which belong to the next frame of the batch or its stride gap) -- only halo
+// lanes and non-centre pixels see them.  EXACT (the last frame of a batch, whose end may be
+// the end of the caller's allocation): the rows whose windows can cross W * H are read byte
+// by byte against num_records = W * H, so nothing past the frame is touched.
+// Luma of the RGB pixel in bytes 0-2 of v (byte 3 ignored), exactly image 0.24.6's to_luma8:
+// (2126 r + 7152 g + 722 b) / 10000.  The weights split as 256 hi + lo with byte-sized hi
+// = (8, 27, 2) and lo = (78, 240, 210) for two v_dot4_u32_u8; x < 2^22, so x / 10000 =
+// (x * 13743896) >> 37 exactly ((13743896 * 10000 - 2^37) * 2^22 < 2^37), the high half from
+// one v_mul_hi_u32_u24.
+__device__ __forceinline__ uint32_t luma_of(uint32_t v) {
+    const uint32_t x = (__builtin_amdgcn_udot4(v, 0x00021B08u, 0u, false) << 8) +
+                       __builtin_amdgcn_udot4(v, 0x00D2F04Eu, 0u, false);
+    return (uint32_t)(((uint64_t)(x & 0xffffffu) * 13743896ull) >> 32) >> 5;
+}
+
+// 16 RGB pixels (48 bytes, d[0..11]) -> their 16 luma bytes.  Pixels 4m .. 4m+3 are exactly
+// dwords 3m .. 3m+2.
+__device__ __forceinline__ u32x4 luma16(const uint32_t (&d)[12]) {
+    u32x4 r;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t p0 = d[3 * m], p1 = alignbyte(d[3 * m + 1], d[3 * m], 3);
+        const uint32_t p2 = alignbyte(d[3 * m + 2], d[3 * m + 1], 2), p3 = d[3 * m + 2] >> 8;
+        r[m] = luma_of(p0) | (luma_of(p1) << 8) | (luma_of(p2) << 16) | (luma_of(p3) << 24);
+    }
+    return r;
+}
+
+template <int LC, bool EXACT>
+__device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& src, int y,
+                                                              int xb) {
+    using RowV = typename LaneRow<LC>::type;
+    // y is wave-uniform, so the row test is scalar: a row outside [0, H) or past the unit's
+    // last row gets an offset of 2^31 + xb, past any frame.  One VALU add per load; a
+    // negative xb in row 0 wraps to >= 2^32 - LC, also out of range (reads 0).  RGB frames:
+    // the same in bytes (3 per pixel).
+    const bool in = y >= 0 && y < (int)src.H && y <= src.ylast;
+    const uint32_t rowoff = in ? (uint32_t)(y * (int)src.W * kPx) : 0x80000000u;
+    const int o = (int)(rowoff + (uint32_t)(xb * kPx));
+    if constexpr (kRgb) {
+        static_assert(LC == 16, "RGB rows are loaded 16 pixels at a time");
+        uint32_t d[12];
+        if (EXACT && y >= src.tail_row) {   // wave-uniform
+#pragma unroll
+            for (int k = 0; k < 12; ++k) d[k] = 0u;
+#pragma unroll
+            for (int k = 0; k < 48; ++k)
+                d[k >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(src.rs, o + k, 0, 0)
+                             << (8 * (k & 3));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(src.rs, o + 16 * k, 0, 0));
+                d[4 * k] = v[0]; d[4 * k + 1] = v[1]; d[4 * k + 2] = v[2]; d[4 * k + 3] = v[3];
+            }
+        }
+        return luma16(d);
+    }
+    if constexpr (EXACT) {
+        if (y >= src.tail_row) {   // wave-uniform
+            RowV r = (RowV)(0u);
+#pragma unroll
+            for (int k = 0; k < LC; ++k)
+                r[k >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(src.rs, o + k, 0, 0)
+                             << (8 * (k & 3));
+            return r;
+        }
+    }
+    if constexpr (LC == 16)
+        return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b128(src.rs, o, 0, 0));
+    else
+        return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b64(src.rs, o, 0, 0));
+}
+
+struct SweepShared {
+    uint32_t* pq;          // kSweepPixelQ FIFO of lane rows with candidates: (row - ys) << 22 |
+                           // lane << 16 | 16-bit mask (bit b = lane column 4 (b & 3) + (b >> 2))
+    uint32_t* stage;       // 64 pixels of the batch being issued: (row - ys) << 10 | strip column
+    uint32_t* bitmap;      // band keypoints: bitmap row i = image row yb + i, words_per_row each
+    uint32_t* slist;       // NMS: the band's keypoints as (bitmap row * W + x) << 12 | score
+    uint32_t* slist_n;     // entries appended (the list, then the spill, then only counted)
+    uint32_t slist_cap;    // kScoreListCap, or 0 when a position does not fit 20 bits
+    uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
+    uint32_t spill_cap;    // slot words (0 with slist_cap 0)
+};
+
+// max-t list entries whose score is computed by the NMS pass: score field kScorePending |
+// polarity (1 = dark); real scores are <= 255
+constexpr uint32_t kScorePending = 0x800u;
+
+struct UnitCtx {
+    RowSource src;
+    uint32_t t, nw;
+    int S;                 // first owned centre column of the strip
+    int p0, p1;            // tested centre rows of the unit (owned rows plus NMS halo rows)
+    int yb;                // image row of bitmap row 0 (band start minus the NMS halo)
+    uint32_t lane;
+    uint32_t head, tail;   // candidate FIFO: entries [head, tail) at pq[i % kSweepPixelQ]
+    int ys;                // first row the unit sweeps (FIFO rows are relative to it)
+    int rowbase;           // (ys - 3) * W: frame offset of the window row y - 3 for FIFO row 0
+    uint32_t flags;        // BandParams::flags (ablation runs only)
+};
+
+// ---------------------------------------------------------------------------------------
+// Full test of a batch of up to 64 queued pixels, one per lane, in two halves: issue pops
+// the batch from the FIFO and starts its loads; evaluate tests the pixels (per-lane VALU
+// segment test) and records keypoints / scores.
+// ---------------------------------------------------------------------------------------
+struct Batch {
+    uint32_t code;         // (row << 10) | strip column
+    uint32_t n;            // pixels in the batch (wave-uniform)
+    bool act;
+    uint32_t a0, a6;       // rows y-3, y+3: 4 bytes from x-1
+    u32x2 a1, a5;          // rows y-2, y+2: 8 bytes from x-2
+    u32x2 a2, a3, a4;      // rows y-1, y, y+1: 8 bytes from x-3
+};
+
+// The 7 row windows around centre (x, y) with o = (y - 3) * W + x.  They stay inside the
+// frame: rows y-3 .. y+3 are rows, and the 1-2 bytes past a row end (rows y-1 .. y+2 only)
+// belong to the next row.
+__device__ __forceinline__ void load_ring_windows(Batch& b, const __amdgpu_buffer_rsrc_t& rs,
+                                                  int o, int W) {
+    if constexpr (kRgb) {
+        // only the 17 window bytes pack_ring reads, each converted from its RGB pixel (one
+        // 12-byte load for three adjacent pixels, a 4-byte load for a single one)
+        auto px = [&](int p) {      // luma of pixel p (4 bytes from 3p; byte 3 unused)
+            return luma_of(__builtin_amdgcn_raw_buffer_load_b32(rs, 3 * p, 0, 0));
+        };
+        auto px3 = [&](int p) {     // luma of pixels p, p+1, p+2 in bytes 0-2
+            const u32x3 v = __builtin_bit_cast(u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, 3 * p, 0, 0));
+            return luma_of(v[0]) | (luma_of(alignbyte(v[1], v[0], 3)) << 8) |
+                   (luma_of(alignbyte(v[2], v[1], 2)) << 16);
+        };
+        b.a0 = px3(o - 1);
+        b.a1.x = px(o - 2 + W);
+        b.a1.y = px(o + 2 + W);
+        b.a2.x = px(o - 3 + 2 * W);
+        b.a2.y = px(o + 3 + 2 * W) << 16;
+        b.a3.x = px(o - 3 + 3 * W) | (px(o + 3 * W) << 24);
+        b.a3.y = px(o + 3 + 3 * W) << 16;
+        b.a4.x = px(o - 3 + 4 * W);
+        b.a4.y = px(o + 3 + 4 * W) << 16;
+        b.a5.x = px(o - 2 + 5 * W);
+        b.a5.y = px(o + 2 + 5 * W);
+        b.a6 = px3(o - 1 + 6 * W);
+        return;
+    }
+    b.a0 = __builtin_amdgcn_raw_buffer_load_b32(rs, o - 1, 0, 0);
+    b.a1 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 2, W, 0));
+    b.a2 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 3, 2 * W, 0));
+    b.a3 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 3, 3 * W, 0));
+    b.a4 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 3, 4 * W, 0));
+    b.a5 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o - 2, 5 * W, 0));
+    b.a6 = __builtin_amdgcn_raw_buffer_load_b32(rs, o - 1, 6 * W, 0);
+}
+
+// Inclusive prefix sum over the wave's 64 lanes (DPP row shifts, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+
+// Maximum over the wave's 64 lanes, in every lane (DPP row shifts, row broadcasts, then lane
+// 63's value read back).
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Position of the j-th (from 0) set bit of a 16-bit mask that has more than j set bits.
+__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t j) {
+    uint32_t bit = 0;
+#pragma unroll
+    for (uint32_t w = 8; w >= 1; w >>= 1) {
+        const uint32_t c = __popc(m & ((1u << w) - 1u));
+        const bool up = j >= c;
+        j -= up ? c : 0u;
+        m = up ? m >> w : m;
+        bit += up ? w : 0u;
+    }
+    return bit;
+}
+
+// Pops the next 64 candidate pixels (fewer only when `force`: a flush) and starts their
+// loads.  The FIFO holds lane rows; the pixels of the first 64 entries are counted with a
+// wave prefix sum, every contributing entry writes its pixels to the staging array in
+// order, and an entry only partly taken keeps its other pixels at the FIFO head.  Without
+// a batch the loads are still issued (all lanes at a harmless address): the pipelined issue
+// points load unconditionally, so that every path through the sweep has the same sequence
+// of loads and the compiler's vmcnt counts stay exact.
+// The FIFO entries a batch is built from (read when the batch is built: a read earlier in
+// the step goes stale when the step's overflow path takes entries).
+struct FifoPeek {
+    uint32_t nent;         // entries read (wave-uniform)
+    uint32_t e;            // this lane's entry (0 past nent)
+};
+__device__ __forceinline__ FifoPeek fifo_peek(const SweepShared& sh, const UnitCtx& u) {
+    FifoPeek f;
+    f.nent = min(u.tail - u.head, 64u);
+    f.e = u.lane < f.nent ? sh.pq[(u.head + u.lane) & (kSweepPixelQ - 1)] : 0u;
+    return f;
+}
+
+template <int LC>
+__device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, bool force,
+                                             const FifoPeek& pk) {
+    static_assert(LC == 16, "16-bit lane masks");
+    Batch b;
+    b.n = 0;
+    b.act = false;
+    b.code = 0;
+    const int W = (int)u.src.W;
+    int o = 3;                                        // pixel (x, y - 3) of centre (3, 3)
+    const uint32_t nent = pk.nent;
+    if (nent != 0) {
+        const uint32_t lane = u.lane;
+        const bool has = lane < nent;
+        const uint32_t e = pk.e;
+        const uint32_t k = (uint32_t)__popc(e & 0xffffu);
+        const uint32_t inc = wave_incl_scan(k);
+        const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+        if (total >= 64u || (force && total != 0u)) {
+            b.n = min(total, 64u);
+            const uint32_t excl = inc - k;
+            uint32_t m = e & 0xffffu;
+#if defined(FDF_BALLOT_EXPAND) || defined(FDF_EXPAND_LOOP)
+            uint32_t pos = excl;
+            const uint32_t rl = (e >> 16) << 4;       // (row - ys) << 10 | lane << 4
+#endif
+#ifdef FDF_BALLOT_EXPAND
+            for (;;) {
+                const bool wr = m != 0u && pos < 64u;
+                if (wave_ballot(wr) == 0) break;
+                if (wr) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    sh.stage[pos] = rl | ((bit & 3u) << 2) | (bit >> 2);
+                    ++pos;
+                }
+            }
+#elif defined(FDF_EXPAND_LOOP)
+            // this lane writes min(k, 64 - excl) pixels; a wave-uniform loop over the most
+            // any lane writes (no per-iteration ballot)
+            const uint32_t cnt = excl < 64u ? min(k, 64u - excl) : 0u;
+            const uint32_t iters = __builtin_amdgcn_readfirstlane(wave_max(cnt));
+            for (uint32_t it = 0; it < iters; ++it) {
+                if (it < cnt) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    sh.stage[pos + it] = rl | ((bit & 3u) << 2) | (bit >> 2);
+                }
+            }
+#else
+            // no per-pixel loop: entry lane e marks the slot its pixels start at, a wave
+            // prefix-max turns the marks into each batch lane's entry, and the lane selects
+            // its bit of that entry's mask (binary search over popcounts)
+            sh.stage[lane] = 0u;
+            if (has && k != 0u && excl < 64u) sh.stage[excl] = lane;
+            // other lanes' stores feed this load: without the (instruction-free) wavefront
+            // fence the compiler forwards the lane's own zero store (per-thread semantics)
+            // and loads only where it stored
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            uint32_t src = sh.stage[lane];
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x111, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x112, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x114, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x118, 0xf, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x142, 0xa, 0xf, false));
+            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x143, 0xc, 0xf, false));
+            const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)e);
+            const uint32_t sx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)excl);
+            {
+                const uint32_t bit = select_bit(se & 0xffffu, lane - sx);
+                // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column
+                if (lane < min(total, 64u))
+                    sh.stage[lane] = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
+            }
+            // the partial entry keeps the bits past the ones taken
+            if (has && excl < 64u && inc > 64u) m &= ~0u << select_bit(m, 64u - excl);
+#endif
+            // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
+            const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
+            if (has && excl < 64u && inc > 64u)
+                sh.pq[(u.head + lane) & (kSweepPixelQ - 1)] = (e & 0xffff0000u) | m;
+            u.head += nfull;
+            b.act = lane < b.n;
+            if (b.act) {
+                const uint32_t sc = sh.stage[lane];
+                b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
+                // rows relative to the unit (< 2^10) times W (< 2^16): a 24-bit multiply
+                o = u.rowbase + (int)__umul24(sc >> 10, (uint32_t)W) + u.S - LC + (int)(sc & 1023u);
+            }
+        }
+    }
+    load_ring_windows(b, u.src.rs, o, W);
+    return b;
+}
+
+template <int LC>
+__device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, bool force) {
+    return issue_batch<LC>(sh, u, force, fifo_peek(sh, u));
+}
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// The ring packed 4 bytes per word (byte j of w[m] = circle pixel 4j + m) and the centre.
+// Circle pixels by window byte: a0 = {15, 0, 1} at bytes 0-2; a1 = {14 @0, 2 @4};
+// a2 = {13 @0, 3 @6}; a3 = {12 @0, c @3, 4 @6}; a4 = {11 @0, 5 @6}; a5 = {10 @0, 6 @4};
+// a6 = {9, 8, 7} at bytes 0-2.  perm selector bytes: 0-3 = low source, 4-7 = high source,
+// 0x0c = zero.
+__device__ __forceinline__ void pack_ring(const Batch& b, uint32_t (&w)[4], uint32_t& c) {
+    w[0] = perm(b.a3.y, b.a0, 0x0c0c0601u) | perm(b.a3.x, b.a6, 0x04010c0cu);   // 0 4 8 12
+    w[1] = perm(b.a4.y, b.a0, 0x0c0c0602u) | perm(b.a2.x, b.a6, 0x04000c0cu);   // 1 5 9 13
+    w[2] = perm(b.a1.y, b.a1.x, 0x000c0c04u) | perm(b.a5.y, b.a5.x, 0x0c00040cu); // 2 6 10 14
+    w[3] = perm(b.a6, b.a2.y, 0x0c0c0602u) | perm(b.a0, b.a4.x, 0x04000c0cu);   // 3 7 11 15
+    c = b.a3.x >> 24;
+}
+
+template <int NMS, int N, int LC>
+__device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
+                                               const LerpConsts& lk, const Batch& b) {
+    if (ablation_flags(u.flags) & kFlagNoEval) {   // ablation: consume the loads, test nothing
+        if (b.act && (b.a0 ^ b.a1.x ^ b.a2.x ^ b.a3.x ^ b.a4.x ^ b.a5.x ^ b.a6) == 0x5a5a5a5au)
+            u.flags |= kFlagNoEval;
+        return;
+    }
+    const int y = (int)(b.code >> 10), cl = (int)(b.code & 1023u);
+    const int x = u.S - LC + cl;
+    uint32_t w[4], c;
+    pack_ring(b, w, c);
+    bool kb, kd;
+    lane_segment_test_packed<N>(c, w, lk, kb, kd);
+    // every queued pixel is a centre of the unit's strip and tested rows (vmask, p0 .. p1)
+    const bool is_kp = b.act && (kb || kd);
+    if (is_kp) atomicOr(&sh.bitmap[__umul24((uint32_t)(y - u.yb), u.nw) + ((uint32_t)x >> 5)], 1u << (x & 31));
+    if constexpr (NMS != kNmsOff) {
+        // scores go to the band's LDS list, past its capacity to the band's slot (global),
+        // past that they are only counted (the band NMS pass then recomputes all scores)
+        const uint64_t bal = wave_ballot(is_kp);
+        if (bal) {
+            uint32_t base = 0;
+            if (u.lane == 0) base = atomicAdd(sh.slist_n, (uint32_t)__popcll(bal));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (is_kp) {
+                uint32_t score;
+                if constexpr (NMS == kNmsMaxThreshold) {
+#ifndef FDF_DEFER_MAXT_SCORE
+                    uint32_t p[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+                    score = score_max_threshold<N>(c, p, kd);
+#else
+                    // deferred (FDF_DEFER_MAXT_SCORE): only keypoints with a neighbouring
+                    // keypoint ever need their score (~28% of a batch's lanes are keypoints),
+                    // so the band NMS pass computes it then, one keypoint per lane
+                    // (nms_scatter).  Measured slower: 1080p max-t +0.9%, 4K max-t +6.6%
+                    // (the NMS pass waits on its gathers)
+                    score = kScorePending | (kd ? 1u : 0u);
+#endif
+                } else {
+                    score = score_sum_abs_packed(c, w, u.t);
+                }
+                const uint32_t idx = base + lanes_below(bal);
+                const uint32_t e = ((__umul24((uint32_t)(y - u.yb), u.src.W) + (uint32_t)x) << 12) | score;
+                if (idx < sh.slist_cap) sh.slist[idx] = e;
+                else if (idx - sh.slist_cap < sh.spill_cap) sh.spill[idx - sh.slist_cap] = e;
+            }
+        }
+    }
+}
+
+// Horizontal/vertical comparison flags of one lane row (bit 7 of each byte, LC pixels).
+template <int LC>
+struct RowFlags {
+    typename LaneRow<LC>::type b, nd;
+};
+
+// Pre-filter comparisons of one lane row (bit 7 of each byte).  FDF_SHARED_LERP: one first
+// lerp for both polarities (fdf_common.h lerp_consts kb0/kd0): `b` flags are a superset of
+// x - c > t and `nd` flags a subset of NOT(x - c < -t), so the cardinal test only gains
+// candidates -- 8 lerps a step fewer, but more candidates on images with exact-threshold
+// steps (measured slower on S1).  Default: the exact comparisons.
+template <int LC>
+__device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>::type& x,
+                                                     const typename LaneRow<LC>::type& nc,
+                                                     const LerpConsts& k) {
+    RowFlags<LC> f;
+#pragma unroll
+    for (int m = 0; m < LC / 4; ++m) {
+#ifdef FDF_SHARED_LERP
+        const uint32_t v = lerp_u8(x[m], nc[m], 0u);
+        f.b[m] = lerp_u8(v, k.kb0, 0);
+        f.nd[m] = lerp_u8(v, k.kd0, 0);
+#else
+        f.b[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rb), k.kb, 0);   // x - c > t
+        f.nd[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rd), k.kd, 0);  // NOT(x - c < -t)
+#endif
+    }
+    return f;
+}
+
+// Test everything queued, now (FIFO overflow, the end of a unit).
+template <int NMS, int N, int LC>
+__device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
+                                            const LerpConsts& lk, bool (&inflight)[kSweepBatchSlots],
+                                            const Batch (&batch)[kSweepBatchSlots]) {
+#pragma unroll
+    for (int q = 0; q < kSweepBatchSlots; ++q) {
+        if (inflight[q]) {
+            evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);
+            inflight[q] = false;
+        }
+    }
+    if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;
+    while (u.tail != u.head) {
+        const Batch b = issue_batch<LC>(sh, u, true);
+        evaluate_batch<NMS, N, LC>(sh, u, lk, b);
+    }
+}
+
+template <int NMS, int N, bool EXACT>
+__device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
+    constexpr int LC = kLaneCols;
+    constexpr int M = LC / 4;
+    constexpr int kIssue = kSweepIssue;
+    using RowV = typename LaneRow<LC>::type;
+    const uint32_t lane = u.lane;
+    const int W = (int)u.src.W;
+    const int xb = u.S - LC + LC * (int)lane;
+    // candidate columns of this lane: the strip's centres (halo lanes 0 and 63 own none)
+    // (bit 8j + m = lane column 4m + j, the order the candidate mask is built in)
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int x = xb + 4 * m + j;
+            if (x >= 3 && x < W - 3 && lane >= 1 && lane <= 62) vmask |= 1u << (8 * j + m);
+        }
+    }
+    const int p0 = u.p0, p1 = u.p1;                    // rows run through the pre-filter
+    const int ys = p0 - 3;                             // first row of vertical comparisons
+    u.ys = ys;
+    u.rowbase = (ys - 3) * W;
+    const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
+    u.src.ylast = p1 + 2;                              // S-row of the last pre-filtered row
+    u.head = u.tail = 0;
+    // kSweepBatchSlots batches in flight, in static slots (issue point q of the K-step loop
+    // body uses slot q % slots), each evaluated slots issue points after it was issued
+    bool inflight[kSweepBatchSlots];
+    Batch batch[kSweepBatchSlots];
+#pragma unroll
+    for (int q = 0; q < kSweepBatchSlots; ++q) inflight[q] = false;
+
+    // One kSweepRing-slot ring of pixel rows: row r in slot (r - ys) % kSweepRing.  At step J
+    // (row yv) it holds rows yv .. yv+K-2 (K = kSweepRing) with yv+4 .. yv+K-2 still loading,
+    // and row yv+K-1 is loaded into the slot of row yv-1, which is dead.  Nothing is copied,
+    // so every slot keeps its registers across loop iterations and no wait is needed for a
+    // register move.  The loop body is K steps, so unit sweeps are whole multiples of K.
+    constexpr int K = kSweepRing;
+    RowV Rw[K];
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
+    RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
+
+    // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
+    // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
+    // their candidates masked: a branch around it costs the zeroing of `cand` on every step.
+#ifdef FDF_LIVE_BRANCH
+#define FDF_LIVE_TEST(l) (l)
+#else
+#define FDF_LIVE_TEST(l) true
+#endif
+#define FDF_SWEEP_STEP(J)                                                                    \
+    {                                                                                        \
+        const int yv = ys + i0 + (J);                                                        \
+        RowV cand = (RowV)(0u);                                                              \
+        Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);                  \
+        const RowV s = Rw[((J) + 3) % K];                  /* row yv + 3 */                  \
+        const RowV c = Rw[(J) % K];                        /* row yv */                      \
+        const RowV nc = ~c;                                                                  \
+        V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
+        const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
+        if (FDF_LIVE_TEST(live)) {                                                           \
+            RowV e;                                                                          \
+            _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
+            e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
+            const RowFlags<LC> h = compare_rows<LC>(e, nc, lk);                              \
+            const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
+            const RowFlags<LC>& vs = V[(J) & 3];                                             \
+            const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
+            _Pragma("unroll") for (int m = 0; m < M; ++m) {                                  \
+                const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);              \
+                const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);          \
+                const uint32_t bn = ~vn.nd[m], bs = vs.b[m], be = h.b[m], bw = ~hndw;        \
+                const uint32_t dn = ~vn.b[m], ds = vs.nd[m], de = h.nd[m], dw = ~hbw;        \
+                uint32_t br, nd;                                                             \
+                if constexpr (N < 12) {                                                      \
+                    br = (bn | bs) & (be | bw);                                              \
+                    nd = (dn & ds) | (de & dw);                                              \
+                } else {                                                                     \
+                    br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
+                    nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
+                }                                                                            \
+                cand[m] = br | ~nd;                                                          \
+            }                                                                                \
+        }                                                                                    \
+        /* the lane row's candidates into the FIFO as one entry: column 4m + j of the */     \
+        /* lane is bit 8j + m of cm, then bit 4j + m of the 16-bit mask */                   \
+        uint32_t cm = 0;                                                                     \
+        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= (cand[m] >> (7 - m)) & (0x01010101u << m); \
+        cm &= live ? vmask : 0u;                                                             \
+        {                                                                                    \
+            const uint32_t cx = cm | (cm >> 4);                                              \
+            const uint32_t m16 = __builtin_amdgcn_perm(cx, cx, 0x0c0c0200u);                 \
+            const bool has = m16 != 0u;                                                      \
+            const uint64_t bal = wave_ballot(has);                                           \
+            if (has)                                                                         \
+                sh.pq[(u.tail + lanes_below(bal)) & (kSweepPixelQ - 1)] =                    \
+                    ((uint32_t)(i0 + (J)) << 22) | (lane << 16) | m16;                       \
+            u.tail += (uint32_t)__popcll(bal);                                               \
+            while (u.tail - u.head > kSweepPixelQ - 64) {                                    \
+                /* dense image: test the oldest pixels now, synchronously */                 \
+                if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                              \
+                else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, true));    \
+            }                                                                                \
+        }                                                                                    \
+        if (((J) % kIssue) == kIssue - 1) {                                                  \
+            /* the batch of this slot is due; issue the next full one into it */             \
+            constexpr int q = ((J) / kIssue) % kSweepBatchSlots;                             \
+            if (inflight[q]) {                                                               \
+                evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);                             \
+                inflight[q] = false;                                                         \
+            }                                                                                \
+            if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                                  \
+            batch[q] = issue_batch<LC>(sh, u, false);                                        \
+            inflight[q] = batch[q].n != 0;                                                   \
+        }                                                                                    \
+    }
+
+    static_assert(K == 8 || K == 12 || K == 16, "ring of 8, 12 or 16 rows");
+    static_assert((K / kIssue) % kSweepBatchSlots == 0 || kSweepBatchSlots == 1,
+                  "issue points per loop body must cycle through the batch slots");
+    for (int i0 = 0; i0 < T; i0 += K) {
+        FDF_SWEEP_STEP(0)
+        FDF_SWEEP_STEP(1)
+        FDF_SWEEP_STEP(2)
+        FDF_SWEEP_STEP(3)
+        FDF_SWEEP_STEP(4)
+        FDF_SWEEP_STEP(5)
+        FDF_SWEEP_STEP(6)
+        FDF_SWEEP_STEP(7)
+        if constexpr (K >= 12) {
+            FDF_SWEEP_STEP(8)
+            FDF_SWEEP_STEP(9)
+            FDF_SWEEP_STEP(10)
+            FDF_SWEEP_STEP(11)
+        }
+        if constexpr (K >= 16) {
+            FDF_SWEEP_STEP(12)
+            FDF_SWEEP_STEP(13)
+            FDF_SWEEP_STEP(14)
+            FDF_SWEEP_STEP(15)
+        }
+    }
+#undef FDF_SWEEP_STEP
+#undef FDF_LIVE_TEST
+    flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
+}
+
+// Three bitmap bits of one bitmap row: columns x-1, x, x+1 (x-1 >= 2, x+1 < W - 3).  Both
+// words are read unconditionally (the bitmap has a pad word after its last row).
+__device__ __forceinline__ uint32_t bits3(const uint32_t* row, int x) {
+    const int xm = x - 1, wi = xm >> 5, sh = xm & 31;
+    const uint64_t v = ((uint64_t)row[wi + 1] << 32) | row[wi];
+    return (uint32_t)(v >> sh) & 7u;
+}
+
+// Raster rank of bitmap position (row, x): keypoints before it in the band's bitmap.
+// rprefix[row] counts the rows above, bprefix[row * nb + k] the words [0, 4k) of the row.
+__device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const uint16_t* bprefix,
+                                                const uint32_t* rprefix, uint32_t nw, uint32_t nb,
+                                                uint32_t row, uint32_t x) {
+    static_assert(kRankBlock == 4, "three block words before the position's word");
+    const uint32_t wi = x >> 5, blk = wi / kRankBlock, w0 = blk * kRankBlock;
+    const uint32_t* rw = bitmap + row * nw;
+    uint32_t r = rprefix[row] + bprefix[row * nb + blk];
+#pragma unroll
+    for (uint32_t j = 0; j < kRankBlock - 1; ++j) {
+        const uint32_t v = rw[min(w0 + j, wi)];         // in-row, read unconditionally
+        r += w0 + j < wi ? __popc(v) : 0u;
+    }
+    return r + __popc(rw[wi] & ((1u << (x & 31)) - 1u));
+}
+
+// Neighbour bits of bitmap position (row, x) among the R2 bitmap rows: bit k of the up /
+// down rows = column x-1+k, mid row bits 0 and 2 (columns x-1, x+1).  Non-zero iff the
+// keypoint has a neighbouring keypoint.
+__device__ __forceinline__ uint32_t neighbour_bits(const uint32_t* bitmap, uint32_t nw, uint32_t R2,
+                                                   uint32_t row, uint32_t x) {
+    return (row > 0 ? bits3(bitmap + (row - 1) * nw, (int)x) : 0u) |
+           (bits3(bitmap + row * nw, (int)x) & 5u) |
+           (row + 1 < R2 ? bits3(bitmap + (row + 1) * nw, (int)x) : 0u);
+}
+
+// Rank prefixes of the band's keypoint bitmap (R2 rows): rprefix[row] = keypoints in the
+// rows above, bprefix[row * nb + k] = keypoints in words [0, 4k) of the row.  Returns the
+// bitmap's keypoint total (every thread).
+__device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint32_t nw,
+                                       uint16_t* bprefix, uint32_t* rprefix, uint32_t* total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    if (nb_blocks <= 32) {
+        // one bitmap row per 16-lane DPP row (or per 32-lane half-wave when it has more than
+        // 16 blocks, e.g. 4K): lane k counts block k, a row_shr scan (+ row_bcast:15 across
+        // the two rows of a half) turns the counts into the row's block prefixes, and the
+        // row's last lane ends with the row total
+        const uint32_t span = nb_blocks <= 16 ? 16u : 32u;
+        for (uint32_t base = 0; base < R2; base += kThreads / span) {
+            const uint32_t row = base + tid / span, k = tid & (span - 1u);
+            const bool act = row < R2 && k < nb_blocks;
+            uint32_t cnt = 0;
+            if (act) {
+                const uint32_t* rw = bitmap + row * nw;
+#pragma unroll
+                for (uint32_t j = 0; j < kRankBlock; ++j)
+                    cnt += kRankBlock * k + j < nw ? __popc(rw[kRankBlock * k + j]) : 0u;
+            }
+            uint32_t inc = cnt;
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xf, 0xf, false);   // row_shr:1
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xf, 0xf, false);   // row_shr:2
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xf, 0xf, false);   // row_shr:4
+            inc += __builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xf, 0xf, false);   // row_shr:8
+            if (span == 32u)
+                inc += __builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xa, 0xf, false);   // row_bcast:15
+            if (act) bprefix[row * nb_blocks + k] = (uint16_t)(inc - cnt);
+            if (row < R2 && k == span - 1u) rprefix[row] = inc;
+        }
+    } else {
+        for (uint32_t i = tid; i < R2 * nb_blocks; i += kThreads) {
+            const uint32_t row = i / nb_blocks, k = i - row * nb_blocks;
+            const uint32_t* rw = bitmap + row * nw;
+            uint32_t cnt = 0;
+            for (uint32_t j = kRankBlock * k; j < min(kRankBlock * k + kRankBlock, nw); ++j)
+                cnt += __popc(rw[j]);
+            bprefix[i] = (uint16_t)cnt;
+        }
+        __syncthreads();
+        for (uint32_t row = tid; row < R2; row += kThreads) {
+            uint32_t acc = 0;
+            for (uint32_t k = 0; k < nb_blocks; ++k) {
+                const uint32_t c = bprefix[row * nb_blocks + k];
+                bprefix[row * nb_blocks + k] = (uint16_t)acc;
+                acc += c;
+            }
+            rprefix[row] = acc;
+        }
+    }
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of the row totals
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < R2; base += 64) {
+            const uint32_t v = base + lane < R2 ? rprefix[base + lane] : 0u;
+            uint32_t incl = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(incl, d, 64);
+                if (lane >= (uint32_t)d) incl += o;
+            }
+            if (base + lane < R2) rprefix[base + lane] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) *total = carry;
+    }
+    __syncthreads();
+    return *total;
+}
+
+// Strict 3x3 maximum of list entry e (src/fast_simd.rs:596-615) against the scores of its
+// neighbouring keypoints, read by raster rank from `sranked`; rows 3 / h-4 and the rows
+// outside the band are reported as suppressed / not compared by the caller's rules below.
+// Returns e with its score field replaced by 1 (suppressed) or 0 (kept).
+__device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap, uint32_t nw,
+                                              uint32_t nb_blocks, uint32_t y0, uint32_t W,
+                                              uint32_t H, const uint16_t* sranked,
+                                              const uint16_t* bprefix, const uint32_t* rprefix) {
+    const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+    const uint32_t y = y0 - 1 + row;
+    const uint32_t own = e & 0xfffu;
+    bool suppressed = y == 3 || y == H - 4;
+    if (own != 0 && !suppressed) {
+        uint32_t mx = 0;
+        const uint32_t mid = bits3(bitmap + row * nw, (int)x);
+        if (mid & 5u) {
+            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+            if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
+            if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
+        }
+#pragma unroll
+        for (int d = -1; d <= 1; d += 2) {
+            const uint32_t nbits = bits3(bitmap + (row + d) * nw, (int)x);
+            if (nbits) {
+                uint32_t r = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row + d, x - 1);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    if ((nbits >> k) & 1u) {
+                        mx = max(mx, (uint32_t)sranked[r]);
+                        ++r;
+                    }
+                }
+            }
+        }
+        suppressed = own <= mx;
+    }
+    return (e & ~0xfffu) | (suppressed ? 1u : 0u);
+}
+
+// Max-threshold score of the keypoint at (x, y) of known polarity, from the frame (the
+// sweep's windows and packing; deferred scores, see evaluate_batch).
+template <int N>
+__device__ __forceinline__ uint32_t keypoint_score_maxt(const __amdgpu_buffer_rsrc_t& rs, int W,
+                                                        int x, int y, bool dark) {
+    Batch b;
+    load_ring_windows(b, rs, (y - 3) * W + x, W);
+    uint32_t w[4], c;
+    pack_ring(b, w, c);
+    uint32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+    return score_max_threshold<N>(c, p, dark);
+}
+
+// Rank-order scatter of list entry e: a keypoint with a neighbouring keypoint puts its score
+// at its raster rank (computing it first when it was deferred); an isolated one is kept
+// without comparison, marked by a zero score.
+template <int NMS, int N>
+__device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitmap, uint32_t nw,
+                                                uint32_t R2, uint32_t nb_blocks, uint32_t W,
+                                                uint32_t y0, uint16_t* sranked,
+                                                const uint16_t* bprefix, const uint32_t* rprefix,
+                                                const __amdgpu_buffer_rsrc_t& frame) {
+    const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+    if (neighbour_bits(bitmap, nw, R2, row, x) == 0) return e & ~0xfffu;
+    if constexpr (NMS == kNmsMaxThreshold) {
+        if (e & kScorePending)
+            e = (e & ~0xfffu) | keypoint_score_maxt<N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), e & 1u);
+    }
+    sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
+    return e;
+}
+
+__device__ __forceinline__ void nms_clear(uint32_t e, uint32_t* bitmap, uint32_t nw, uint32_t W) {
+    if ((e & 0xfffu) == 1u) {
+        const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+        atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
+    }
+}
+
+__device__ __forceinline__ bool in_band_rows(uint32_t e, uint32_t W, uint32_t R2) {
+    const uint32_t row = (e >> 12) / W;
+    return row != 0 && row != R2 - 1;                 // bitmap rows 0, R2-1: neighbours only
+}
+
+// Band NMS (src/fast_simd.rs:589-616) from the band's score list, in place on the keypoint
+// bitmap (bitmap rows 0 and rows + 1 are the rows just outside the band, neighbours only).
+// The list holds every keypoint of the bitmap once; its scores are scattered into raster
+// rank order, then each keypoint of the band's own rows reads its neighbours' scores by
+// rank, and the suppressed ones are cleared once every comparison has read the bitmap.
+// Rows 3 and h-4 are never output (:590-592, :342).
+//   n <= cap: the list is in LDS and the ranked scores go to the FIFO area.
+//   n > cap (the band_nms_spill variant): entries past the LDS list were appended to the
+//   band's slot (`spill`); the LDS entries move to registers (kSpillPer per thread), so the
+//   ranked scores can use the whole FIFO + staging + list area.
+template <int NMS, int N>
+__device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                             uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
+                             uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags,
+                             __amdgpu_buffer_rsrc_t frame) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
+    if (flags & kFlagNmsPrefixOnly) return;
+    for (uint32_t i = tid; i < n; i += kThreads)
+        slist[i] = nms_scatter<NMS, N>(slist[i], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
+                                       rprefix, frame);
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) {
+        const uint32_t e = slist[i];
+        if (in_band_rows(e, W, R2))
+            slist[i] = nms_entry(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) nms_clear(slist[i], bitmap, nw, W);
+    __syncthreads();
+}
+
+constexpr uint32_t kSpillPer = kScoreListCap / kThreads;
+
+template <int NMS, int N>
+__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+                               uint32_t H, const uint32_t* slist, uint32_t cap, uint32_t* spill,
+                               uint32_t n, uint16_t* sranked, uint16_t* bprefix, uint32_t* rprefix,
+                               uint32_t* total, __amdgpu_buffer_rsrc_t frame) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
+    uint32_t ent[kSpillPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j) ent[j] = slist[tid + j * kThreads];
+    band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);   // barriers: list area free
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j)
+        ent[j] = nms_scatter<NMS, N>(ent[j], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
+                                     rprefix, frame);
+    for (uint32_t i = tid; i < n - cap; i += kThreads)
+        spill[i] = nms_scatter<NMS, N>(spill[i], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
+                                       rprefix, frame);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j)
+        if (in_band_rows(ent[j], W, R2))
+            ent[j] = nms_entry(ent[j], bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+    for (uint32_t i = tid; i < n - cap; i += kThreads) {
+        const uint32_t e = spill[i];
+        if (in_band_rows(e, W, R2))
+            spill[i] = nms_entry(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kSpillPer; ++j) nms_clear(ent[j], bitmap, nw, W);
+    for (uint32_t i = tid; i < n - cap; i += kThreads) nms_clear(spill[i], bitmap, nw, W);
+    __syncthreads();
+}
+
+// Score of the keypoint at (x, y) recomputed from the frame (the same windows, packing and
+// score functions as the sweep's full test).
+template <int NMS, int N>
+__device__ __forceinline__ uint32_t keypoint_score(const __amdgpu_buffer_rsrc_t& rs, int W, int x,
+                                                   int y, const LerpConsts& lk, uint32_t t) {
+    Batch b;
+    load_ring_windows(b, rs, (y - 3) * W + x, W);
+    uint32_t w[4], c;
+    pack_ring(b, w, c);
+    if constexpr (NMS == kNmsSumAbsolute) {
+        return score_sum_abs_packed(c, w, t);
+    } else {
+        bool kb, kd;
+        lane_segment_test_packed<N>(c, w, lk, kb, kd);
+        uint32_t p[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+        return score_max_threshold<N>(c, p, kd);
+    }
+}
+
+// Band NMS for bands too dense for the list and its spill (more keypoints than the LDS
+// list plus the slot hold, or a frame too wide for 20-bit list positions): no scores are
+// stored.  Each keypoint with a neighbouring keypoint recomputes its own and its neighbours'
+// scores; the kill masks go to the slot (one word per bitmap word, exactly the slot's size)
+// and are applied after.  Rows 3 and h-4 are never output (:590-592, :342); the caller
+// clears them.
+template <int NMS, int N>
+__device__ void band_nms_dense(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0,
+                               uint32_t W, uint32_t* slot, __amdgpu_buffer_rsrc_t frame,
+                               LerpConsts lk, uint32_t t) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t R2 = rows + 2;
+    for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) {
+        const uint32_t row = wi / nw;
+        uint32_t bits = bitmap[wi], kill = 0;
+        while (bits) {
+            const uint32_t bit = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const uint32_t x = (wi - row * nw) * 32 + bit;
+            const int y = (int)(y0 - 1 + row);
+            const uint32_t mid = bits3(bitmap + row * nw, (int)x) & 5u;
+            const uint32_t up = bits3(bitmap + (row - 1) * nw, (int)x);
+            const uint32_t dn = bits3(bitmap + (row + 1) * nw, (int)x);
+            if ((mid | up | dn) == 0) continue;
+            const uint32_t own = keypoint_score<NMS, N>(frame, (int)W, (int)x, y, lk, t);
+            bool suppressed = false;
+#pragma unroll
+            for (int d = -1; d <= 1; ++d) {
+                const uint32_t nbits = d < 0 ? up : (d == 0 ? mid : dn);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    if (!suppressed && ((nbits >> k) & 1u) &&
+                        keypoint_score<NMS, N>(frame, (int)W, (int)x - 1 + k, y + d, lk, t) >= own)
+                        suppressed = true;
+                }
+            }
+            if (suppressed) kill |= 1u << bit;
+        }
+        slot[wi - nw] = kill;
+    }
+    __syncthreads();
+    for (uint32_t wi = nw + tid; wi < (R2 - 1) * nw; wi += kThreads) bitmap[wi] &= ~slot[wi - nw];
+    __syncthreads();
+}
+
+// The band (task) a workgroup sweeps.  XCD-aware static task mapping: each XCD takes a contiguous range of bands (raster
+    // order), so consecutive bands of a frame land on one XCD (its L2 then serves the halo
+    // rows two neighbouring bands share).  Within its range an XCD dispatches the frames'
+    // full bands first and their (shorter) last bands at the end, where they fill the grid's
+    // tail.
+__device__ __forceinline__ uint32_t band_task(const BandParams& P) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
+    const uint32_t c0 = k8 * q8 + min(k8, r8), j = b >> 3;
+    uint32_t task = c0 + j;
+#ifndef FDF_RASTER_DISPATCH
+    {
+        const uint32_t c1 = c0 + q8 + (k8 < r8 ? 1u : 0u);
+        const uint32_t B = P.bands_per_frame;
+        if (B > 1) {
+            const uint32_t s0 = c0 / B, s1 = c1 / B;          // last bands before c0 / c1
+            const uint32_t n_full = (c1 - c0) - (s1 - s0);
+            if (j < n_full) {
+                const uint32_t u = (c0 - s0) + j;              // index among full bands
+                task = (u / (B - 1)) * B + u % (B - 1);
+            } else {
+                task = (s0 + (j - n_full)) * B + (B - 1);
+            }
+        }
+    }
+#endif
+    return task;
+}
+
+// Sweeps band `task`, runs its NMS and writes its slot; returns the band's keypoint count.
+template <int NMS, int N>
+__device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* smem_raw, uint32_t task) {
+    constexpr int LC = kLaneCols;
+    const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, NMS);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63;
+    const uint32_t W = P.width, H = P.height, nw = P.words_per_row;
+    constexpr uint32_t halo = NMS == kNmsOff ? 0u : 1u;
+    const uint32_t frame = task / P.bands_per_frame;
+    const uint32_t band = task - frame * P.bands_per_frame;
+    const uint32_t y0 = 3 + band * P.rows;
+    const uint32_t rows = min(P.rows, H - 3 - y0);
+
+    uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap);
+    uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.misc);
+    if (P.threshold >= 255) return 0;                                // no pixel can pass
+    uint32_t* unit_ctr = wave_sum + kWaves;
+    for (uint32_t i = tid; i <= (rows + 2 * halo) * nw; i += kThreads) bitmap[i] = 0;   // + pad
+    if (tid == 0) {
+        unit_ctr[0] = 0;
+        unit_ctr[1] = 0;
+    }
+    __syncthreads();
+
+    SweepShared sh;
+    sh.pq = reinterpret_cast<uint32_t*>(smem_raw + L.pq + wave * L.wave_bytes);
+    sh.stage = reinterpret_cast<uint32_t*>(smem_raw + L.stage + wave * 64 * 4);
+    sh.bitmap = bitmap;
+    sh.slist = reinterpret_cast<uint32_t*>(smem_raw + L.slist);
+    sh.slist_n = unit_ctr + 1;
+    // list positions are (bitmap row * W + x) in 20 bits
+    sh.slist_cap = (uint64_t)(rows + 2 * halo) * W <= (1u << 20) ? kScoreListCap : 0u;
+    sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
+    sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
+
+    UnitCtx u;
+    const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
+    u.src.W = W;
+    u.src.H = H;
+    const bool last_frame = frame + 1 == P.ntasks / P.bands_per_frame;
+    // frames before the last may be read up to 15 pixels past their end (inside the batch)
+    const __amdgpu_buffer_rsrc_t rs_pad = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(img), 0, (int)((W * H + 15) * kPx), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_exact = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(img), 0, (int)(W * H * kPx), 0x00020000);
+    u.t = P.threshold;
+    u.nw = nw;
+    u.yb = (int)(y0 - halo);
+    u.lane = lane;
+    u.flags = ablation_flags(P.flags);
+    const LerpConsts lk = lerp_consts(P.threshold);
+
+    const uint32_t nunits = P.nstrips * P.nsub;
+    const uint32_t sub_rows = (rows + P.nsub - 1) / P.nsub;
+    // units are handed out dynamically: a wave that finishes early takes the next one
+    // instead of idling at the workgroup barrier
+    if (!(ablation_flags(P.flags) & kFlagNoPrefilter)) {
+        for (;;) {
+            uint32_t unit = 0;
+            if (lane == 0) unit = atomicAdd(unit_ctr, 1u);
+            unit = __builtin_amdgcn_readfirstlane(unit);
+            if (unit >= nunits) break;
+            const uint32_t strip = unit % P.nstrips, sub = unit / P.nstrips;
+            u.S = (int)strip * strip_cols(LC);
+            {   // first row whose last lane's window can end past W * H
+                const int last_end = u.S - LC + LC * 64;
+                const int num = (int)(W * H) - last_end;
+                u.src.tail_row = num < 0 ? 0 : num / (int)W + 1;
+            }
+            const int r0 = (int)(y0 + sub * sub_rows);
+            const int r1 = (int)min(y0 + (sub + 1) * sub_rows, y0 + rows);
+            if (r0 >= r1) continue;
+            // NMS: the band's first and last units also test the rows just outside the band
+            u.p0 = (halo && sub == 0 && r0 > 3) ? r0 - 1 : r0;
+            u.p1 = (halo && r1 == (int)(y0 + rows) && r1 < (int)H - 3) ? r1 + 1 : r1;
+            // rows the sweep loads: up to p1 + 2
+            if (last_frame && u.p1 + 2 >= u.src.tail_row) {
+                u.src.rs = rs_exact;
+                sweep_unit<NMS, N, true>(sh, u, lk);
+            } else {
+                u.src.rs = rs_pad;
+                sweep_unit<NMS, N, false>(sh, u, lk);
+            }
+        }
+    }
+    __syncthreads();
+
+    const uint32_t nwords = rows * nw;
+    if constexpr (NMS != kNmsOff) {
+        const uint32_t n = *sh.slist_n;
+        if (ablation_flags(P.flags) & kFlagNoNms) {
+        } else if (n <= sh.slist_cap) {
+            band_nms_lds<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, n,
+                                 reinterpret_cast<uint16_t*>(smem_raw + L.pq),
+                                 reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                                 reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+                                 ablation_flags(P.flags), rs_exact);
+        } else if (n - sh.slist_cap <= sh.spill_cap && n <= L.nms_area_entries) {
+            // more keypoints than the LDS list holds: the rest were appended to the slot
+            band_nms_spill<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap, sh.spill, n,
+                                   reinterpret_cast<uint16_t*>(smem_raw + L.pq),
+                                   reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
+                                   reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
+                                   rs_exact);
+        } else {
+            band_nms_dense<NMS, N>(bitmap, rows, nw, y0, W,
+                                   reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
+                                   rs_exact, lk, P.threshold);
+            // rows 3 and h - 4 keep no keypoints (they were neighbours only)
+            for (uint32_t y : {3u, H - 4u}) {
+                if (y < y0 || y >= y0 + rows) continue;
+                for (uint32_t w = tid; w < nw; w += kThreads) bitmap[(y - y0 + 1) * nw + w] = 0;
+            }
+            __syncthreads();
+        }
+        // the band's own rows are now its keep-bits
+    }
+    const uint32_t* keep = bitmap + halo * nw;
+
+    // ---- count keep-bits and write the band slot
+#ifdef FDF_EMIT_PER_THREAD
+    const uint32_t per = (nwords + kThreads - 1) / kThreads;
+    const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);
+    uint32_t mine = 0;
+    for (uint32_t w = w_lo; w < w_hi; ++w) mine += __popc(keep[w]);
+    uint32_t incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += o;
+    }
+    if (lane == 63) wave_sum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const uint32_t v = wave_sum[w];
+        before += (uint32_t)w < wave ? v : 0u;
+        total += v;
+    }
+    if (ablation_flags(P.flags) & kFlagNoEmit) return total;
+    uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
+    if (total <= P.slot_bytes / 8) {
+        uint2* pts = reinterpret_cast<uint2*>(slot);
+        uint32_t idx = before + incl - mine;
+        for (uint32_t w = w_lo; w < w_hi; ++w) {
+            uint32_t bits = keep[w];
+            const uint32_t r = w / nw;
+            const uint32_t xb = (w - r * nw) * 32;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                pts[idx++] = make_uint2(xb + bit, y0 + r);
+            }
+        }
+    } else {
+        uint32_t* words = reinterpret_cast<uint32_t*>(slot);
+        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
+    }
+#else
+    // Each wave owns a contiguous quarter of the bitmap and sweeps it 64 words per round (lane
+    // = word): the word reads are independent and conflict-free, and a wave prefix sum of the
+    // words' keypoint counts places the round's points consecutively in the slot.
+    const uint32_t wq = (nwords + kWaves - 1) / kWaves;
+    const uint32_t wb = min(wave * wq, nwords), we = min(wb + wq, nwords);
+    uint32_t mine = 0;
+    for (uint32_t w = wb + lane; w < we; w += 64) mine += __popc(keep[w]);
+    const uint32_t wave_total = __builtin_amdgcn_readlane(wave_incl_scan(mine), 63);
+    if (lane == 0) wave_sum[wave] = wave_total;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const uint32_t v = wave_sum[w];
+        before += (uint32_t)w < wave ? v : 0u;
+        total += v;
+    }
+    if (ablation_flags(P.flags) & kFlagNoEmit) return total;
+    uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
+    if (total <= P.slot_bytes / 8) {
+        uint2* pts = reinterpret_cast<uint2*>(slot);
+        uint32_t o = before;
+        for (uint32_t w0 = wb; w0 < we; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            uint32_t bits = w < we ? keep[w] : 0u;
+            const uint32_t c = __popc(bits);
+            const uint32_t inc = wave_incl_scan(c);
+            uint32_t idx = o + inc - c;
+            o += __builtin_amdgcn_readlane(inc, 63);
+            const uint32_t r = w / nw;
+            const uint32_t xb = (w - r * nw) * 32;
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                pts[idx++] = make_uint2(xb + bit, y0 + r);
+            }
+        }
+    } else {
+        uint32_t* words = reinterpret_cast<uint32_t*>(slot);
+        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
+    }
+#endif
+    return total;
+}
+
+// Occupancy target: kSweepWavesPerEU waves per SIMD (4: 128 VGPRs each, 2: 256).
+template <int NMS, int N>
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(kSweepWavesPerEU, kSweepWavesPerEU)))
+void fast_sweep_kernel(BandParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    const uint32_t task = band_task(P);
+    const uint32_t total = sweep_band<NMS, N>(P, smem_raw, task);
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        P.counts[task] = total;
+        if (P.group_sums) atomicAdd(&P.group_sums[task / P.tasks_per_group], total);
+    }
+#ifdef FDF_FUSED_COMPACT
+    if (P.fused) {
+        // fused compaction (small grids): every band publishes its slot and count, and the
+        // last one to finish (a ticket) orders them all
+        __threadfence();
+        __syncthreads();
+        uint32_t* last = reinterpret_cast<uint32_t*>(smem_raw);
+        if (tid == 0) *last = atomicAdd(P.ticket, 1u) == P.ntasks - 1u ? 1u : 0u;
+        __syncthreads();
+        if (*last) {
+            __threadfence();
+            __syncthreads();
+            CompactShared& sm = *reinterpret_cast<CompactShared*>(smem_raw + 16);
+            const uint32_t ngroups = (P.ntasks + P.compact.tasks_per_group - 1) / P.compact.tasks_per_group;
+            for (uint32_t g = 0; g < ngroups; ++g) {
+                compact_group(P.compact, g, sm);
+                __syncthreads();
+            }
+            if (tid == 0) *P.ticket = 0u;           // for the next launch
+        }
+    }
+#endif
+}
+
+typedef void (*SweepKernelFn)(BandParams);
+
+template <int NMS>
+static SweepKernelFn pick_sweep_n(uint32_t n) {
+    switch (n) {
+        case 9: return fast_sweep_kernel<NMS, 9>;
+        case 10: return fast_sweep_kernel<NMS, 10>;
+        case 11: return fast_sweep_kernel<NMS, 11>;
+        case 12: return fast_sweep_kernel<NMS, 12>;
+        case 13: return fast_sweep_kernel<NMS, 13>;
+        case 14: return fast_sweep_kernel<NMS, 14>;
+        case 15: return fast_sweep_kernel<NMS, 15>;
+        case 16: return fast_sweep_kernel<NMS, 16>;
+        default: return nullptr;
+    }
+}
+
+hipError_t launch(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream) {
+    SweepKernelFn fn = nullptr;
+    switch (nms) {
+        case kNmsOff: fn = pick_sweep_n<kNmsOff>(n); break;
+        case kNmsMaxThreshold: fn = pick_sweep_n<kNmsMaxThreshold>(n); break;
+        case kNmsSumAbsolute: fn = pick_sweep_n<kNmsSumAbsolute>(n); break;
+        default: break;
+    }
+    if (!fn) return hipErrorInvalidValue;
+    const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, nms);
+    if (L.total > kSweepMaxLds) return hipErrorInvalidValue;
+    if (L.total > kMaxLds) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)L.total);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
+    return hipGetLastError();
+}
+
+}  // namespace FDF_SWEEP_NS
+}  // namespace fdfk

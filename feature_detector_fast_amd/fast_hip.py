@@ -260,6 +260,33 @@ def detect_device(frames, config, out, offsets, stream=None, device=None):
     check(rc, "fdf_detect_device")
 
 
+def detect_device_rgb(frames, config, out, offsets, stream=None, device=None):
+    """detect_device for RGB8 frames: ``frames`` a contiguous (F, H, W, 3) uint8 CUDA tensor;
+    the detector converts pixels to luma (image 0.24.6 to_luma8) as it loads them
+    (fdf_detect_device_rgb), so no grey copy is written."""
+    import torch
+
+    if frames.dim() != 4 or frames.shape[3] != 3 or frames.dtype != torch.uint8 or \
+            not frames.is_contiguous():
+        raise ValueError("frames must be a contiguous (F, H, W, 3) uint8 tensor")
+    if not frames.is_cuda or not out.is_cuda or not offsets.is_cuda:
+        raise ValueError("detect_device_rgb needs CUDA (HIP) tensors")
+    if offsets.dtype != torch.int64 or offsets.numel() < frames.shape[0] + 1:
+        raise ValueError("offsets must be int64 with F+1 entries")
+    if out.dim() != 2 or out.shape[1] != 2 or out.element_size() != 4 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (cap, 2) 32-bit tensor")
+    dev = frames.device.index if device is None else device
+    cfg = _to_c_config(config)
+    ctx = context(dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(frames.device)
+    f, h, w = frames.shape[:3]
+    rc = _native.load().fdf_detect_device_rgb(
+        ctx.handle, frames.data_ptr(), f, w, h, 3 * h * w, ctypes.byref(cfg), out.data_ptr(),
+        out.shape[0], offsets.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+    check(rc, "fdf_detect_device_rgb")
+
+
 def keypoint_scores(img, points, config, device=0):
     """u16 NMS scores of the given centres (extension: the reference's Point has no score).
     ``config.non_maximal_supression`` picks MaxThreshold (src/fast_simd.rs:623-718, window =
@@ -347,5 +374,5 @@ __all__ = ["NORTH", "EAST", "SOUTH", "WEST", "circle", "calculate_offsets", "con
            "shard_contexts", "capacity_guess",
            "detect_array", "detector", "detector_batch", "detect_device", "keypoint_scores",
            "detect_scored_array", "detector_scored", "detector_batch_scored", "score_device",
-           "detect_rgb_array", "detector_rgb", "rgb_to_luma",
+           "detect_rgb_array", "detector_rgb", "rgb_to_luma", "detect_device_rgb",
            "NonMaximalSuppression"]

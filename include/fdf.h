@@ -197,6 +197,20 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
                       uint64_t* d_frame_offsets, void* stream);
 
 /*
+ * fdf_detect_device for RGB8 frames (rows of 3 * width bytes, frame f at
+ * d_frames + f * frame_stride_bytes): the detector converts each loaded pixel with image
+ * 0.24.6's to_luma8 -- (2126 r + 7152 g + 722 b) / 10000 -- so the keypoints are those of
+ * fdf_rgb_to_luma_device followed by fdf_detect_device, with no grey frames written
+ * (src/main.rs:58, tests/compare.rs:33).  3 * width * height < 2^31.  It needs no grey
+ * buffer but is slower than the two passes, which the host RGB entry
+ * points use.
+ */
+int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
+                          uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
+                          const fdf_config* cfg, fdf_point* d_out, uint64_t cap,
+                          uint64_t* d_frame_offsets, void* stream);
+
+/*
  * Scores for given points (extension: the reference's Point carries no score; these are the
  * u16 values its NMS compares, src/fast_simd.rs:623-718 and :722-749).  Host in/out,
  * synchronous.  `nms` selects the score: MaxThreshold (window = cfg->count) or SumAbsolute

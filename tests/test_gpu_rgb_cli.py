@@ -97,3 +97,48 @@ def test_cli_default_nms_is_sum_absolute(tmp_path):
     got = workloads.read_points(out_png.replace(".png", ".txt"))
     img = workloads.read_pgm(os.path.join(GOLD, "screenshot315_grey.pgm"))
     assert np.array_equal(got, oracle.detect(img, 16, 9, 2))
+
+
+@pytest.mark.parametrize("nms", [0, 1, 2])
+@pytest.mark.parametrize("geometry", [0, 1])
+def test_rgb_device_batch_fused(nms, geometry):
+    """fdf_detect_device_rgb (luma converted inside the detector's row and window loads)
+    equals fdf_rgb_to_luma_device + fdf_detect_device on a batch of colour frames -- random
+    colours, a colour-tinted S1 frame, odd sizes, the last frame read exactly -- and the oracle
+    on two frames; with the batch's own geometry and with the tall bands."""
+    import torch
+
+    rng = np.random.default_rng(31 + nms)
+    H, W = 301, 517
+    frames = []
+    for i in range(6):
+        if i % 2:
+            g = workloads.s1_frame(i, W, H).astype(np.int32)
+            tint = rng.integers(-40, 41, 3)
+            frames.append(np.clip(g[..., None] + tint, 0, 255).astype(np.uint8))
+        else:
+            frames.append(rng.integers(0, 256, (H, W, 3), dtype=np.uint8))
+    rgb = torch.from_numpy(np.stack(frames)).cuda()
+    grey = torch.empty((6, H, W), dtype=torch.uint8, device="cuda")
+    cfg = Config(12, 9, NonMaximalSuppression(nms))
+    cap = 6 * H * W
+    out_a = torch.empty((cap, 2), dtype=torch.int32, device="cuda")
+    out_b = torch.empty((cap, 2), dtype=torch.int32, device="cuda")
+    offs_a = torch.zeros(7, dtype=torch.int64, device="cuda")
+    offs_b = torch.zeros(7, dtype=torch.int64, device="cuda")
+    ctx = fast_hip.context(0)
+    ctx.set_geometry(geometry)
+    try:
+        fast_hip.detect_device_rgb(rgb, cfg, out_a, offs_a)
+        fast_hip.rgb_to_luma(rgb, grey)
+        fast_hip.detect_device(grey, cfg, out_b, offs_b)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_geometry(0)
+    assert torch.equal(offs_a, offs_b)
+    n = int(offs_a[-1])
+    assert torch.equal(out_a[:n], out_b[:n])
+    o = offs_a.cpu().numpy()
+    for f in (1, 5):
+        want = oracle.detect(oracle.rgb_to_luma(frames[f]), 12, 9, nms)
+        assert np.array_equal(out_a[o[f]:o[f + 1]].cpu().numpy().astype(np.uint32), want), f
