@@ -46,6 +46,13 @@ struct fdf_ctx {
     uint32_t* d_sums = nullptr;         // 2 x fdfk::kMaxGroupSums, then the ticket
     int sums_parity = 0;
     bool sums_dirty = false;            // a launch failed: re-zero before the next use
+    // NMS keypoint density feedback (band height): the compaction writes the last finished
+    // launch's pre-NMS keypoint total to host-mapped memory, tagged with its launch number
+    uint64_t* h_stats = nullptr;        // pinned, mapped; *h_stats = seq << 32 | total
+    uint64_t* d_stats = nullptr;        // its device address
+    uint32_t stats_seq = 0;
+    struct LaunchInfo { uint32_t seq = 0, t = 0, n = 0, nms = 0, w = 0; double pixels = 0; };
+    LaunchInfo hist[8];
     // cross-stream ordering: the device work of the last enqueue (on any stream) completes
     // at `done`; the next enqueue on another stream waits for it first
     hipEvent_t done = nullptr;
@@ -131,7 +138,7 @@ struct Geometry {
 
 
 Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
-                       uint64_t min_tasks) {
+                       uint64_t min_tasks, double density) {
     Geometry g;
     const uint32_t sc = (uint32_t)fdfk::strip_cols(fdfk::kLaneCols);
     g.nstrips = (w - 3 + sc - 1) / sc;
@@ -158,9 +165,17 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     // shortest sweep (one ring block per unit) for the lowest latency.  min_tasks = 1
     // (fdf_ctx_set_geometry, tests) gives a small job the full-size geometry (tall bands,
     // long units); the keypoints are the same either way.
+    // NMS: when an earlier launch of this configuration measured the keypoint density, keep
+    // a band's expected keypoints (x1.5) within the LDS score list, so that bands do not
+    // spill (4K t=8 n=12 SAD: 27-row bands instead of 43, 0.747 -> 0.732 ms)
+    uint32_t max_rows = 256;
+    if (nms && density > 0.0) {
+        const double rows = (double)fdfk::kScoreListCap / (1.5 * density * (double)w) - 2.0;
+        max_rows = rows < (double)g.nsub ? g.nsub : (rows > 256.0 ? 256u : (uint32_t)rows);
+    }
     double best = -1.0;
     g.R = 0;
-    for (uint32_t R = g.nsub; R <= 256 && R < centre_rows + g.nsub; R += g.nsub) {
+    for (uint32_t R = g.nsub; R <= max_rows && R < centre_rows + g.nsub; R += g.nsub) {
         if (fdfk::make_sweep_layout(R, nw, nms).total > budget) break;
         const uint64_t tasks = (uint64_t)n_frames * ((centre_rows + R - 1) / R);
         if (tasks < min_tasks) break;
@@ -183,8 +198,31 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream, bool rgb = false) {
+    double density = 0.0;
+    if (cfg->nms) {
+        if (!ctx->h_stats) {
+            void* hp = nullptr;
+            void* dp = nullptr;
+            if (hipHostMalloc(&hp, 64, hipHostMallocMapped) == hipSuccess &&
+                hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
+                ctx->h_stats = static_cast<uint64_t*>(hp);
+                ctx->d_stats = static_cast<uint64_t*>(dp);
+                *ctx->h_stats = 0;
+            } else if (hp) {
+                (void)hipHostFree(hp);
+            }
+        }
+        if (ctx->h_stats) {
+            const uint64_t v = *reinterpret_cast<volatile uint64_t*>(ctx->h_stats);
+            const uint32_t seq = (uint32_t)(v >> 32);
+            const fdf_ctx::LaunchInfo& li = ctx->hist[seq % 8];
+            if (seq != 0 && li.seq == seq && li.t == cfg->threshold && li.n == cfg->count &&
+                li.nms == cfg->nms && li.w == w && li.pixels > 0)
+                density = (double)(uint32_t)v / li.pixels;
+        }
+    }
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms,
-                                       ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks);
+                                       ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks, density);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
     if (fdfk::make_sweep_layout(R, nw, cfg->nms).total > fdfk::kSweepMaxLds)
@@ -273,6 +311,24 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.group_sums = grouped ? sums_now : nullptr;
     p.tasks_per_group = tpg;
     p.ticket = ctx->d_sums + 2 * fdfk::kMaxGroupSums;
+    p.kp_stats = nullptr;
+    c.kp_stats = nullptr;
+    c.stats_out = nullptr;
+    c.stats_seq = 0;
+    if (cfg->nms && ctx->h_stats) {
+        const uint32_t seq = ++ctx->stats_seq == 0 ? ++ctx->stats_seq : ctx->stats_seq;
+        fdf_ctx::LaunchInfo& li = ctx->hist[seq % 8];
+        li.seq = seq;
+        li.t = cfg->threshold;
+        li.n = cfg->count;
+        li.nms = cfg->nms;
+        li.w = w;
+        li.pixels = (double)n_frames * (double)w * (double)(h - 6);
+        p.kp_stats = ctx->d_sums + 2 * fdfk::kMaxGroupSums + 1;
+        c.kp_stats = p.kp_stats;
+        c.stats_out = ctx->d_stats;
+        c.stats_seq = seq;
+    }
     p.fused = fused ? 1u : 0u;
     p.compact = c;
     hipEvent_t* ev = nullptr;
@@ -390,6 +446,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (size_t)total, ctx->stream))) return rc;
         c.out = ctx->d_out;
         c.cap = ctx->out_points;
+        c.kp_stats = nullptr;           // already reported (and reset) by the first compaction
         if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
             hipEventRecord(ctx->done, ctx->stream) != hipSuccess)
             return FDF_ERR_DEVICE;
@@ -551,6 +608,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_sums);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         if (ctx->done) (void)hipEventDestroy(ctx->done);
+        if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
         (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;

@@ -52,6 +52,12 @@ __device__ __forceinline__ void compact_group(const CompactParams& P, uint32_t g
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t T = P.tasks_per_group;
+    if (g == 0 && tid == 0 && P.kp_stats) {
+        // the launch's keypoint density for the host's next band-height choice
+        const uint32_t v = *P.kp_stats;
+        *P.kp_stats = 0u;
+        *P.stats_out = ((uint64_t)P.stats_seq << 32) | v;
+    }
     const uint32_t first = g * T;
     const uint32_t ntask_here = min(T, P.ntasks - first);
     const uint32_t task = first + tid;

@@ -148,6 +148,9 @@ struct CompactParams {
     uint64_t* frame_offsets;         // frames + 1 entries
     const uint32_t* group_sums;      // per-group sums of this launch (NULL: sum the counts)
     uint32_t* next_sums;             // zeroed here for the next launch (kMaxGroupSums entries)
+    uint32_t* kp_stats;              // NMS: the detector's keypoint total (read and reset here)
+    uint64_t* stats_out;             // host-mapped: stats_seq << 32 | that total
+    uint32_t stats_seq;
 };
 
 struct BandParams {
@@ -168,6 +171,7 @@ struct BandParams {
     uint32_t tasks_per_group;
     uint32_t* ticket;            // fused compaction: bands finished (the last one resets it)
     uint32_t fused;              // 1: the last workgroup runs `compact` (ntasks <= kFusedCompactTasks)
+    uint32_t* kp_stats;          // NMS: += each band's keypoints before suppression (NULL: off)
     CompactParams compact;
 };
 

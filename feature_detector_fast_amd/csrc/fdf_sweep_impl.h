@@ -1113,6 +1113,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     const uint32_t nwords = rows * nw;
     if constexpr (NMS != kNmsOff) {
         const uint32_t n = *sh.slist_n;
+        if (tid == 0 && P.kp_stats) atomicAdd(P.kp_stats, n);
         if (ablation_flags(P.flags) & kFlagNoNms) {
         } else if (n <= sh.slist_cap) {
             band_nms_lds<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, n,
