@@ -440,10 +440,16 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
                 uint32_t score;
                 if constexpr (NMS == kNmsMaxThreshold) {
 #ifndef FDF_DEFER_MAXT_SCORE
+#ifdef FDF_MAXT_PACKED
+                    // over u16 pairs (fdf_common.h): 1080p +0.6%, 4K max-t -1.8% (A/B
+                    // profiles/r02/ab_maxt_packed_*), so not the default
+                    score = score_max_threshold_packed<N>(c, w, kd);
+#else
                     uint32_t p[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
                     score = score_max_threshold<N>(c, p, kd);
+#endif
 #else
                     // deferred (FDF_DEFER_MAXT_SCORE): only keypoints with a neighbouring
                     // keypoint ever need their score (~28% of a batch's lanes are keypoints),
