@@ -38,7 +38,8 @@ EXPORTED_SYMBOLS = (
     "fdf_pipeline_destroy", "fdf_pipeline_acquire", "fdf_pipeline_submit", "fdf_pipeline_push",
     "fdf_pipeline_collect", "fdf_ctx_set_geometry", "fdf_ctx_timing_samples", "fdf_fetch_last",
     "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
-    "fdf_detect_device_rgb",
+    "fdf_detect_device_rgb", "fdf_circle", "fdf_calculate_offsets", "fdf_score_rings",
+    "fdf_score_rings_device",
 )
 
 
@@ -125,6 +126,15 @@ def load():
     lib.fdf_detect_device.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp]
     lib.fdf_detect_device_rgb.restype = ctypes.c_int
     lib.fdf_detect_device_rgb.argtypes = [vp, vp, u32, u32, u32, u64, cfgp, vp, u64, vp, vp]
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    lib.fdf_circle.restype = None
+    lib.fdf_circle.argtypes = [i32p, i32p]
+    lib.fdf_calculate_offsets.restype = None
+    lib.fdf_calculate_offsets.argtypes = [u32, i32p]
+    lib.fdf_score_rings.restype = ctypes.c_int
+    lib.fdf_score_rings.argtypes = [vp, vp, vp, sz, cfgp, vp]
+    lib.fdf_score_rings_device.restype = ctypes.c_int
+    lib.fdf_score_rings_device.argtypes = [vp, vp, vp, u64, cfgp, vp, vp]
     lib.fdf_score_points.restype = ctypes.c_int
     lib.fdf_score_points.argtypes = [vp, vp, u32, u32, sz, cfgp, vp, sz, vp]
     lib.fdf_detect_scored.restype = ctypes.c_int

@@ -859,6 +859,81 @@ int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t
     return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
 }
 
+// ---- ring-level helpers (src/fast_simd.rs:69-110, :623, :722) ---------------------------
+
+static constexpr int32_t kCircleDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+static constexpr int32_t kCircleDy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
+
+void fdf_circle(int32_t dx[16], int32_t dy[16]) {
+    for (int i = 0; i < 16; ++i) {
+        if (dx) dx[i] = kCircleDx[i];
+        if (dy) dy[i] = kCircleDy[i];
+    }
+}
+
+void fdf_calculate_offsets(uint32_t width, int32_t offsets[16]) {
+    if (!offsets) return;
+    for (int i = 0; i < 16; ++i)   // same i32 arithmetic as the reference (wraps like it)
+        offsets[i] = (int32_t)((uint32_t)kCircleDy[i] * width + (uint32_t)kCircleDx[i]);
+}
+
+static int check_ring_args(const fdf_config* cfg) {
+    if (!cfg) return FDF_ERR_ARG;
+    if (cfg->nms != FDF_NMS_MAX_THRESHOLD && cfg->nms != FDF_NMS_SUM_ABSOLUTE) return FDF_ERR_NMS;
+    if (cfg->nms == FDF_NMS_MAX_THRESHOLD && (cfg->count < 9 || cfg->count > 16))
+        return FDF_ERR_COUNT;
+    return FDF_OK;
+}
+
+static inline uint8_t ring_count(const fdf_config* cfg) {
+    return cfg->nms == FDF_NMS_MAX_THRESHOLD ? cfg->count : 9;   // SAD ignores the count
+}
+
+int fdf_score_rings_device(fdf_ctx* ctx, const uint8_t* d_centers, const uint8_t* d_rings,
+                           uint64_t n_rings, const fdf_config* cfg, uint16_t* d_scores,
+                           void* stream) {
+    if (!ctx || n_rings > 0xffffffffull) return FDF_ERR_ARG;
+    int rc = check_ring_args(cfg);
+    if (rc) return rc;
+    if (n_rings == 0) return FDF_OK;
+    if (!d_centers || !d_rings || !d_scores || ((uintptr_t)d_rings & 15u)) return FDF_ERR_ARG;
+    DeviceGuard guard(ctx->device);
+    const hipError_t e = fdfk::launch_score_rings(d_centers, d_rings, (uint32_t)n_rings, cfg->nms,
+                                                  cfg->threshold, ring_count(cfg), d_scores,
+                                                  stream ? (hipStream_t)stream : ctx->stream);
+    return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
+}
+
+int fdf_score_rings(fdf_ctx* ctx, const uint8_t* centers, const uint8_t* rings, size_t n_rings,
+                    const fdf_config* cfg, uint16_t* out_scores) {
+    if (!ctx || n_rings > 0xffffffffull) return FDF_ERR_ARG;
+    int rc = check_ring_args(cfg);
+    if (rc) return rc;
+    if (n_rings == 0) return FDF_OK;
+    if (!centers || !rings || !out_scores) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    ctx->last.valid = false;              // d_in / d_out are reused below
+    wait_done(ctx);
+    const size_t ring_bytes = n_rings * 16;
+    if ((rc = ensure(ctx, &ctx->d_in, &ctx->in_bytes, ring_bytes + n_rings, ctx->stream))) return rc;
+    if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (n_rings + 3) / 4, ctx->stream))) return rc;
+    uint16_t* d_scores = reinterpret_cast<uint16_t*>(ctx->d_out);
+    hipError_t e = hipMemcpyAsync(ctx->d_in, rings, ring_bytes, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->d_in + ring_bytes, centers, n_rings, hipMemcpyHostToDevice,
+                           ctx->stream);
+    if (e == hipSuccess)
+        e = fdfk::launch_score_rings(ctx->d_in + ring_bytes, ctx->d_in, (uint32_t)n_rings,
+                                     cfg->nms, cfg->threshold, ring_count(cfg), d_scores,
+                                     ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(out_scores, d_scores, n_rings * sizeof(uint16_t), hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
+}
+
 // ---- multi-device batch: contiguous frame shards, one host thread per context ----------
 
 int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* data,

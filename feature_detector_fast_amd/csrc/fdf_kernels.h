@@ -181,6 +181,9 @@ hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream
 hipError_t launch_sweep_rgb(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
 hipError_t launch_rgb_to_luma(const uint8_t* rgb, uint32_t n_frames, uint32_t pixels,
                               uint64_t rgb_frame_stride, uint8_t* grey, hipStream_t stream);
+hipError_t launch_score_rings(const uint8_t* centers, const uint8_t* rings, uint32_t nrings,
+                              uint32_t nms, uint32_t t, uint32_t n, uint16_t* out,
+                              hipStream_t stream);
 hipError_t launch_score_points(const uint8_t* img, uint32_t width, const uint2* pts,
                                uint32_t npts, uint32_t nms, uint32_t t, uint32_t n,
                                uint16_t* out, hipStream_t stream);

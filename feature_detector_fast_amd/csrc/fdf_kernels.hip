@@ -6,6 +6,8 @@
 //   when the kernel starts), then copies its bands' points to their final positions.
 // score_points_kernel -- the reference's two NMS score functions on given points
 //   (extension: fdf_score_points).
+// score_rings_kernel -- the same on (centre, 16 circle pixels) tuples through the detector's
+//   own score functions (fdf_score_rings; src/fast_simd.rs:623, :722).
 // rgb_to_luma_kernel -- RGB8 -> grey exactly as image 0.24.6's to_luma8, which the
 //   reference's callers apply before detect (src/main.rs:58, tests/compare.rs:33).
 #include <hip/hip_runtime.h>
@@ -29,35 +31,41 @@ __global__ __launch_bounds__(kCompactTasks) void compact_kernel(CompactParams P)
 // Point scoring (extension, fdf_score_points): literal formulas of the reference's score
 // functions, valid for any point, one thread per point.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint16_t score_point(const uint8_t* img, uint32_t W, uint2 pt,
-                                                uint32_t nms, uint32_t t, uint32_t n) {
-    const int c = img[(uint64_t)pt.y * W + pt.x];
+// Literal reference formulas on a ring (d_i = c - p_i), valid for any ring.
+__device__ __forceinline__ uint32_t score_ring_literal(int c, const int (&p)[16], uint32_t nms,
+                                                       uint32_t t, uint32_t n) {
     int d[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-        d[i] = c - (int)img[(uint64_t)((int)pt.y + circle_dy(i)) * W + (int)pt.x + circle_dx(i)];
-    uint32_t score;
+    for (int i = 0; i < 16; ++i) d[i] = c - p[i];
     if (nms == kNmsSumAbsolute) {    // src/fast_simd.rs:722-749
         uint32_t sb = 0, sd = 0;
         for (int i = 0; i < 16; ++i) {
             sb += (uint32_t)max(d[i] - (int)t, 0);
             sd += (uint32_t)max(-d[i] - (int)t, 0);
         }
-        score = max(sb, sd);
-    } else {                          // src/fast_simd.rs:623-718
-        int hi = -32768, lo = 32767;
-        for (int kk = 0; kk < 16; ++kk) {
-            int mn = 32767, mx = -32768;
-            for (uint32_t i = 0; i < n; ++i) {
-                mn = min(mn, d[(kk + i) & 15]);
-                mx = max(mx, d[(kk + i) & 15]);
-            }
-            hi = max(hi, mn);
-            lo = min(lo, mx);
-        }
-        score = (uint32_t)min(abs(hi), abs(lo));
+        return max(sb, sd);
     }
-    return (uint16_t)score;
+    int hi = -32768, lo = 32767;      // src/fast_simd.rs:623-718
+    for (int kk = 0; kk < 16; ++kk) {
+        int mn = 32767, mx = -32768;
+        for (uint32_t i = 0; i < n; ++i) {
+            mn = min(mn, d[(kk + i) & 15]);
+            mx = max(mx, d[(kk + i) & 15]);
+        }
+        hi = max(hi, mn);
+        lo = min(lo, mx);
+    }
+    return (uint32_t)min(abs(hi), abs(lo));
+}
+
+__device__ __forceinline__ uint16_t score_point(const uint8_t* img, uint32_t W, uint2 pt,
+                                                uint32_t nms, uint32_t t, uint32_t n) {
+    const int c = img[(uint64_t)pt.y * W + pt.x];
+    int p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        p[i] = img[(uint64_t)((int)pt.y + circle_dy(i)) * W + (int)pt.x + circle_dx(i)];
+    return (uint16_t)score_ring_literal(c, p, nms, t, n);
 }
 
 __global__ __launch_bounds__(256) void score_points_kernel(const uint8_t* img, uint32_t W,
@@ -85,6 +93,69 @@ __global__ __launch_bounds__(256) void score_frames_kernel(const uint8_t* frames
     for (uint64_t k = b + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < e;
          k += (uint64_t)gridDim.x * blockDim.x)
         out[k] = score_point(img, W, pts[k], nms, t, n);
+}
+
+// ---------------------------------------------------------------------------------------
+// Ring scoring (fdf_score_rings; the reference's pub ring functions src/fast_simd.rs:623
+// and :722, which take a centre and the 16 circle pixels).  SumAbsolute goes through the
+// detector's own score_sum_abs_packed; MaxThreshold through the detector's segment test
+// (t = 0: the polarity of an arc of N pixels brighter / darker than the centre) and its
+// score_max_threshold<N>, and the literal formula for rings with no such arc (the detector
+// never scores those).  Ring k is 16 bytes at rings + 16 k (16-byte aligned).
+// ---------------------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(256) void score_rings_kernel(const uint8_t* centers,
+                                                          const uint4* rings, uint32_t nrings,
+                                                          uint32_t nms, uint32_t t,
+                                                          uint16_t* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nrings) return;
+    const uint4 r = rings[k];
+    const uint32_t c = centers[k];
+    const uint32_t wd[4] = {r.x, r.y, r.z, r.w};   // byte j of wd[q] = pixel 4q + j
+    uint32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = (wd[i >> 2] >> (8 * (i & 3))) & 0xffu;
+    uint32_t score;
+    if (nms == kNmsSumAbsolute) {
+        uint32_t w[4];   // byte j of w[m] = pixel 4j + m (the detector's packed ring)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            w[m] = p[m] | (p[m + 4] << 8) | (p[m + 8] << 16) | (p[m + 12] << 24);
+        score = score_sum_abs_packed(c, w, t);
+    } else {
+        bool bright, dark;
+        lane_segment_test<N>(c, p, lerp_consts(0), bright, dark);
+        if (bright || dark) {
+            score = score_max_threshold<N>(c, p, dark);
+        } else {
+            int q[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) q[i] = (int)p[i];
+            score = score_ring_literal((int)c, q, nms, t, N);
+        }
+    }
+    out[k] = (uint16_t)score;
+}
+
+hipError_t launch_score_rings(const uint8_t* centers, const uint8_t* rings, uint32_t nrings,
+                              uint32_t nms, uint32_t t, uint32_t n, uint16_t* out,
+                              hipStream_t stream) {
+    if (nrings == 0) return hipSuccess;
+    if (((uintptr_t)rings & 15u) != 0 || n < 9 || n > 16) return hipErrorInvalidValue;
+    const dim3 grid((nrings + 255) / 256), block(256);
+    const uint4* r = reinterpret_cast<const uint4*>(rings);
+    switch (n) {
+#define FDF_RING_CASE(NN)                                                                     \
+    case NN:                                                                                 \
+        hipLaunchKernelGGL(score_rings_kernel<NN>, grid, block, 0, stream, centers, r, nrings, \
+                           nms, t, out);                                                     \
+        break;
+        FDF_RING_CASE(9) FDF_RING_CASE(10) FDF_RING_CASE(11) FDF_RING_CASE(12)
+        FDF_RING_CASE(13) FDF_RING_CASE(14) FDF_RING_CASE(15) FDF_RING_CASE(16)
+#undef FDF_RING_CASE
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream) {

@@ -303,6 +303,64 @@ def keypoint_scores(img, points, config, device=0):
     return scores
 
 
+def _ring_config(score, t, n):
+    return _native.FdfConfig(t, n, int(score))
+
+
+def score_rings(centers, rings, score, threshold=0, consecutive=9, device=0):
+    """u16 scores of (centre, 16 circle pixels) rings on the GPU (fdf_score_rings).
+    ``score`` is NonMaximalSuppression.MaxThreshold (src/fast_simd.rs:623, window
+    ``consecutive``) or SumAbsolute (:722, ``threshold``); ``rings`` is (K, 16) uint8 in
+    circle() order, ``centers`` (K,) uint8."""
+    c = np.ascontiguousarray(np.asarray(centers, dtype=np.uint8).reshape(-1))
+    r = np.ascontiguousarray(np.asarray(rings, dtype=np.uint8).reshape(-1, 16))
+    if r.shape[0] != c.shape[0]:
+        raise ValueError("centers and rings differ in length")
+    if not 0 <= int(threshold) <= 255:
+        raise ValueError("threshold must fit u8")
+    cfg = _ring_config(score, threshold, consecutive)
+    out = np.zeros(c.shape[0], dtype=np.uint16)
+    rc = _native.load().fdf_score_rings(context(device).handle, c.ctypes.data, r.ctypes.data,
+                                        c.shape[0], ctypes.byref(cfg), out.ctypes.data)
+    check(rc, "fdf_score_rings")
+    return out
+
+
+def keypoint_score_max_threshold(base_v, pixels, consecutive):
+    """src/fast_simd.rs:623 on one ring (16 circle pixels), computed on the GPU."""
+    return int(score_rings([base_v], [pixels], NonMaximalSuppression.MaxThreshold,
+                           consecutive=consecutive)[0])
+
+
+def keypoint_score_sum_abs_difference(pixels, center, threshold):
+    """src/fast_simd.rs:722 on one ring with the masks its callers build from ``threshold``
+    (:1213-1222), computed on the GPU."""
+    return int(score_rings([center], [pixels], NonMaximalSuppression.SumAbsolute,
+                           threshold=threshold)[0])
+
+
+def score_rings_device(centers, rings, scores, score, threshold=0, consecutive=9,
+                       stream=None, device=None):
+    """Device-resident fdf_score_rings_device: torch uint8 (K,) centres and (K, 16) rings,
+    int16/uint16-sized (K,) scores tensor, all on one GPU; asynchronous on ``stream``."""
+    import torch
+    if rings.dim() != 2 or rings.shape[1] != 16 or centers.numel() != rings.shape[0] \
+            or scores.numel() < rings.shape[0]:
+        raise ValueError("rings must be (K, 16) with K centres and K scores")
+    if not (centers.is_contiguous() and rings.is_contiguous() and scores.is_contiguous()):
+        raise ValueError("tensors must be contiguous")
+    if scores.element_size() != 2:
+        raise ValueError("scores must be a 16-bit tensor")
+    dev = rings.device.index if device is None else device
+    cfg = _ring_config(score, threshold, consecutive)
+    if stream is None:
+        stream = torch.cuda.current_stream(rings.device)
+    rc = _native.load().fdf_score_rings_device(
+        context(dev).handle, centers.data_ptr(), rings.data_ptr(), rings.shape[0],
+        ctypes.byref(cfg), scores.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+    check(rc, "fdf_score_rings_device")
+
+
 def detect_scored_array(img, config, device=0):
     """Keypoints with scores: ((K, 2) uint32 (x, y) in raster order, (K,) uint16 scores).
     The score is the one the configured NMS suppresses with, max-threshold when NMS is off
@@ -375,4 +433,5 @@ __all__ = ["NORTH", "EAST", "SOUTH", "WEST", "circle", "calculate_offsets", "con
            "detect_array", "detector", "detector_batch", "detect_device", "keypoint_scores",
            "detect_scored_array", "detector_scored", "detector_batch_scored", "score_device",
            "detect_rgb_array", "detector_rgb", "rgb_to_luma", "detect_device_rgb",
-           "NonMaximalSuppression"]
+           "score_rings", "score_rings_device", "keypoint_score_max_threshold",
+           "keypoint_score_sum_abs_difference", "NonMaximalSuppression"]

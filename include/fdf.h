@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FDF_ABI_VERSION 2
+#define FDF_ABI_VERSION 3
 
 /* Status codes.  Shapes the reference maps to an empty Vec return FDF_OK with 0 points. */
 enum fdf_status {
@@ -209,6 +209,38 @@ int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_fram
                           uint32_t width, uint32_t height, uint64_t frame_stride_bytes,
                           const fdf_config* cfg, fdf_point* d_out, uint64_t cap,
                           uint64_t* d_frame_offsets, void* stream);
+
+/*
+ * Ring-level helpers, the reference's pub items of src/fast_simd.rs:
+ *   FDF_NORTH..FDF_WEST   :69-72   circle indices of the four cardinal pixels
+ *   fdf_circle            :79-98   (dx, dy) of the 16 circle pixels, index 0 north, clockwise
+ *   fdf_calculate_offsets :104-110 dy * width + dx (i32, as the reference computes it)
+ * Either output pointer of fdf_circle may be NULL.  Host-only, no context needed.
+ */
+#define FDF_NORTH 0
+#define FDF_EAST 4
+#define FDF_SOUTH 8
+#define FDF_WEST 12
+void fdf_circle(int32_t dx[16], int32_t dy[16]);
+void fdf_calculate_offsets(uint32_t width, int32_t offsets[16]);
+
+/*
+ * Ring scores, the reference's keypoint_score_max_threshold(base_v, pixels, consecutive)
+ * (src/fast_simd.rs:623) and keypoint_score_sum_abs_difference(pixels, centers, is_above,
+ * is_below, threshold) (:722) with the masks its callers build (:282, test :1213-1222:
+ * is_above = p > sat(c + t), is_below = p < sat(c - t)).  Ring k is centers[k] and the 16
+ * circle pixels rings[16 k .. 16 k + 16) in fdf_circle order.  cfg->nms picks the function:
+ * MaxThreshold (consecutive = cfg->count, 9..16) or SumAbsolute (threshold = cfg->threshold).
+ * Runs on the GPU through the detector's own score functions (see fdf_kernels.hip), for any
+ * ring.  fdf_score_rings: host in/out, synchronous; invalidates fdf_fetch_last's result.
+ * fdf_score_rings_device: device pointers, d_rings 16-byte aligned, asynchronous on
+ * `stream` (NULL = the context's stream).
+ */
+int fdf_score_rings(fdf_ctx* ctx, const uint8_t* centers, const uint8_t* rings, size_t n_rings,
+                    const fdf_config* cfg, uint16_t* out_scores);
+int fdf_score_rings_device(fdf_ctx* ctx, const uint8_t* d_centers, const uint8_t* d_rings,
+                           uint64_t n_rings, const fdf_config* cfg, uint16_t* d_scores,
+                           void* stream);
 
 /*
  * Scores for given points (extension: the reference's Point carries no score; these are the

@@ -8,6 +8,11 @@
 //   Config::detect(&img)            src/lib.rs:56-58     fdf::Config::detect(img)
 //   detect(&img, &config)           src/lib.rs:62-64     fdf::detect(img, config)
 //   fast_simd::detector(img, cfg)   src/fast_simd.rs:847 fdf::fast_hip::detector(img, cfg)
+//   fast_simd::NORTH..WEST          src/fast_simd.rs:69  fdf::fast_hip::NORTH..WEST
+//   fast_simd::circle()             src/fast_simd.rs:79  fdf::fast_hip::circle()
+//   fast_simd::calculate_offsets(w) src/fast_simd.rs:104 fdf::fast_hip::calculate_offsets(w)
+//   keypoint_score_max_threshold    src/fast_simd.rs:623 fdf::fast_hip::keypoint_score_max_threshold
+//   keypoint_score_sum_abs_difference :722               fdf::fast_hip::keypoint_score_sum_abs_difference
 //   image::GrayImage                (image 0.24.6)       fdf::GrayView (borrowed row-major u8)
 //
 // Where the reference panics (n < 9, n > 16, degenerate sizes) these throw fdf::Error.
@@ -15,10 +20,12 @@
 // fdf::set_device() was called), so the free functions stay pure calls like the reference's.
 #pragma once
 
+#include <array>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "fdf.h"
@@ -120,6 +127,46 @@ namespace fast_hip {
 inline size_t capacity_guess(const GrayView& img) {
     const size_t px = (size_t)img.width * img.height;
     return px / 64 > 4096 ? px / 64 : 4096;
+}
+
+constexpr size_t NORTH = FDF_NORTH;
+constexpr size_t EAST = FDF_EAST;
+constexpr size_t SOUTH = FDF_SOUTH;
+constexpr size_t WEST = FDF_WEST;
+
+using CircleOffsets = std::array<int32_t, 16>;
+
+inline std::array<std::pair<int32_t, int32_t>, 16> circle() {
+    int32_t dx[16], dy[16];
+    fdf_circle(dx, dy);
+    std::array<std::pair<int32_t, int32_t>, 16> c;
+    for (int i = 0; i < 16; ++i) c[i] = {dx[i], dy[i]};
+    return c;
+}
+
+inline CircleOffsets calculate_offsets(uint32_t width) {
+    CircleOffsets o;
+    fdf_calculate_offsets(width, o.data());
+    return o;
+}
+
+// Ring scores on the GPU (fdf_score_rings), one ring per call as the reference's functions;
+// batch through fdf_score_rings for many.  `pixels` are the 16 circle pixels in circle() order.
+inline uint16_t keypoint_score_max_threshold(uint8_t base_v, const std::array<uint8_t, 16>& pixels,
+                                             uint8_t consecutive) {
+    fdf_config c{0, consecutive, FDF_NMS_MAX_THRESHOLD};
+    uint16_t s = 0;
+    check(fdf_score_rings(thread_context().get(), &base_v, pixels.data(), 1, &c, &s),
+          "fdf_score_rings");
+    return s;
+}
+inline uint16_t keypoint_score_sum_abs_difference(const std::array<uint8_t, 16>& pixels,
+                                                  uint8_t center, uint8_t threshold) {
+    fdf_config c{threshold, 9, FDF_NMS_SUM_ABSOLUTE};
+    uint16_t s = 0;
+    check(fdf_score_rings(thread_context().get(), &center, pixels.data(), 1, &c, &s),
+          "fdf_score_rings");
+    return s;
 }
 
 // Drop-in for fast_simd::detector: result in raster order, bit-identical to the reference.

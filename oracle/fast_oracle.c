@@ -196,3 +196,12 @@ void fdf_oracle_score_points(const uint8_t* img, size_t stride, const uint32_t* 
                            : fdf_oracle_score_max_threshold(c, c16, n);
     }
 }
+
+/* Scores of (centre, ring) tuples (test helper for the GPU's fdf_score_rings): kind as
+ * fdf_oracle_score_points; ring k is rings[16 k .. 16 k + 16) in circle order. */
+void fdf_oracle_score_rings(const uint8_t* centers, const uint8_t* rings, size_t n_rings,
+                            uint8_t kind, uint8_t t, uint8_t n, uint16_t* out) {
+    for (size_t k = 0; k < n_rings; ++k)
+        out[k] = kind == 2 ? fdf_oracle_score_sum_abs(centers[k], rings + 16 * k, t)
+                           : fdf_oracle_score_max_threshold(centers[k], rings + 16 * k, n);
+}

@@ -36,6 +36,10 @@ int64_t fdf_oracle_detect(const uint8_t* img, uint32_t w, uint32_t h, size_t str
 void fdf_oracle_score_points(const uint8_t* img, size_t stride, const uint32_t* xy,
                              size_t n_pts, uint8_t kind, uint8_t t, uint8_t n, uint16_t* out);
 
+/* Scores of (centre, 16 circle pixels) tuples: kind as fdf_oracle_score_points. */
+void fdf_oracle_score_rings(const uint8_t* centers, const uint8_t* rings, size_t n_rings,
+                            uint8_t kind, uint8_t t, uint8_t n, uint16_t* out);
+
 #ifdef __cplusplus
 }
 #endif

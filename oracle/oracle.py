@@ -54,6 +54,9 @@ def _load():
         lib.fdf_oracle_score_points.restype = None
         lib.fdf_oracle_score_points.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                                 ctypes.c_size_t, u8, u8, u8, ctypes.c_void_p]
+        lib.fdf_oracle_score_rings.restype = None
+        lib.fdf_oracle_score_rings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                               u8, u8, u8, ctypes.c_void_p]
         _lib = lib
     return _lib
 
@@ -104,6 +107,18 @@ def score_points(img, points, kind, t, n):
     if pts.shape[0]:
         _load().fdf_oracle_score_points(img.ctypes.data, img.shape[1], pts.ctypes.data,
                                         pts.shape[0], int(kind), int(t), int(n), out.ctypes.data)
+    return out
+
+
+def score_rings(centers, rings, kind, t, n):
+    """Oracle scores (uint16) of rings ((K, 16) uint8, circle order) around `centers` (K,):
+    kind 1 max-threshold with window n, kind 2 SAD with threshold t."""
+    c = np.ascontiguousarray(np.asarray(centers, dtype=np.uint8).reshape(-1))
+    r = np.ascontiguousarray(np.asarray(rings, dtype=np.uint8).reshape(-1, 16))
+    out = np.zeros(c.shape[0], dtype=np.uint16)
+    if c.shape[0]:
+        _load().fdf_oracle_score_rings(c.ctypes.data, r.ctypes.data, c.shape[0], int(kind),
+                                       int(t), int(n), out.ctypes.data)
     return out
 
 

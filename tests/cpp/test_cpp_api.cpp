@@ -65,6 +65,18 @@ int main(int argc, char** argv) {
     } catch (const fdf::Error& e) {
         if (e.status() != FDF_ERR_COUNT) ++failures;
     }
+    // ring helpers: circle / offsets (src/fast_simd.rs:79-110) and the score KAT of
+    // test_47_115_score_calc (src/fast_simd.rs:919-948): centre 17, n = 9 -> 20
+    namespace fh = fdf::fast_hip;
+    if (fh::circle()[fh::EAST] != std::make_pair(3, 0) || fh::calculate_offsets(w)[fh::NORTH] != -3 * (int32_t)w) {
+        std::fprintf(stderr, "circle / offsets differ\n");
+        ++failures;
+    }
+    const std::array<uint8_t, 16> ring{37, 37, 39, 39, 37, 42, 43, 16, 14, 13, 15, 16, 15, 38, 37, 38};
+    if (fh::keypoint_score_max_threshold(17, ring, 9) != 20) {
+        std::fprintf(stderr, "max-t KAT: %u != 20\n", fh::keypoint_score_max_threshold(17, ring, 9));
+        ++failures;
+    }
     std::printf("off=%zu maxt=%zu failures=%d\n", got_off.size(), got_maxt.size(), failures);
     return failures ? 1 : 0;
 }
