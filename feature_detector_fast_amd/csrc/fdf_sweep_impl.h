@@ -182,6 +182,11 @@ struct UnitCtx {
     int ys;                // first row the unit sweeps (FIFO rows are relative to it)
     int rowbase;           // (ys - 3) * W: frame offset of the window row y - 3 for FIFO row 0
     uint32_t flags;        // BandParams::flags (ablation runs only)
+#ifndef FDF_NO_KP_QUEUE
+    // max-t keypoint queue (one entry per lane, kq_n < 64 entries, wave-uniform): the packed
+    // ring and pos << 12 | dark << 8 | centre of keypoints whose score is not computed yet
+    uint32_t kq_w[4], kq_c, kq_n;
+#endif
 };
 
 // ---------------------------------------------------------------------------------------
@@ -316,6 +321,8 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             b.n = min(total, 64u);
             const uint32_t excl = inc - k;
             uint32_t m = e & 0xffffu;
+            uint32_t scode = 0;
+            (void)scode;
 #if defined(FDF_BALLOT_EXPAND) || defined(FDF_EXPAND_LOOP)
             uint32_t pos = excl;
             const uint32_t rl = (e >> 16) << 4;       // (row - ys) << 10 | lane << 4
@@ -364,9 +371,9 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             const uint32_t sx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)excl);
             {
                 const uint32_t bit = select_bit(se & 0xffffu, lane - sx);
-                // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column
-                if (lane < min(total, 64u))
-                    sh.stage[lane] = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
+                // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column,
+                // kept in the lane (no LDS round trip: the lane reads only its own pixel)
+                scode = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
             }
             // the partial entry keeps the bits past the ones taken
             if (has && excl < 64u && inc > 64u) m &= ~0u << select_bit(m, 64u - excl);
@@ -378,7 +385,11 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             u.head += nfull;
             b.act = lane < b.n;
             if (b.act) {
+#if defined(FDF_BALLOT_EXPAND) || defined(FDF_EXPAND_LOOP)
                 const uint32_t sc = sh.stage[lane];
+#else
+                const uint32_t sc = scode;
+#endif
                 b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
                 // rows relative to the unit (< 2^10) times W (< 2^16): a 24-bit multiply
                 o = u.rowbase + (int)__umul24(sc >> 10, (uint32_t)W) + u.S - LC + (int)(sc & 1023u);
@@ -411,6 +422,35 @@ __device__ __forceinline__ void pack_ring(const Batch& b, uint32_t (&w)[4], uint
     c = b.a3.x >> 24;
 }
 
+// Appends one score-list entry per active lane: the band's LDS list, past its capacity the
+// band's slot (global), past that only counted.
+__device__ __forceinline__ void append_scores(const SweepShared& sh, const UnitCtx& u, bool act,
+                                              uint64_t bal, uint32_t e) {
+    uint32_t base = 0;
+    if (u.lane == 0) base = atomicAdd(sh.slist_n, (uint32_t)__popcll(bal));
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (act) {
+        const uint32_t idx = base + lanes_below(bal);
+        if (idx < sh.slist_cap) sh.slist[idx] = e;
+        else if (idx - sh.slist_cap < sh.spill_cap) sh.spill[idx - sh.slist_cap] = e;
+    }
+}
+
+#ifndef FDF_NO_KP_QUEUE
+// Scores the first n entries of the max-t keypoint queue (one per lane) and lists them.
+template <int N>
+__device__ __forceinline__ void score_kp_queue(const SweepShared& sh, UnitCtx& u, uint32_t n) {
+    const bool act = u.lane < n;
+    const uint32_t c = u.kq_c & 0xffu;
+    uint32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = (u.kq_w[i & 3] >> (8 * (i >> 2))) & 0xffu;
+    const uint32_t score = score_max_threshold<N>(c, p, (u.kq_c >> 8) & 1u);
+    append_scores(sh, u, act, n >= 64 ? ~0ull : (1ull << n) - 1ull,
+                  (u.kq_c & 0xfffff000u) | score);
+}
+#endif
+
 template <int NMS, int N, int LC>
 __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
                                                const LerpConsts& lk, const Batch& b) {
@@ -428,6 +468,44 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
     // every queued pixel is a centre of the unit's strip and tested rows (vmask, p0 .. p1)
     const bool is_kp = b.act && (kb || kd);
     if (is_kp) atomicOr(&sh.bitmap[__umul24((uint32_t)(y - u.yb), u.nw) + ((uint32_t)x >> 5)], 1u << (x & 31));
+#ifndef FDF_NO_KP_QUEUE
+    if constexpr (NMS == kNmsMaxThreshold) {
+        // ~28% of a batch's lanes are keypoints (S1), and the max-t score is ~100 VALU on
+        // every lane: keypoints move into the wave's queue (lane q + rank, via the staging
+        // array -- free between a batch's issue and the next -- and ds_bpermute), and a full
+        // queue of 64 is scored at once.  Keypoints past the 64th wrap to lanes 0.. of the
+        // next queue; the same permuted values serve both.
+        const uint64_t bal = wave_ballot(is_kp);
+        if (bal) {
+            const uint32_t k = (uint32_t)__popcll(bal);
+            const uint32_t q = u.kq_n;
+            if (is_kp) sh.stage[(q + lanes_below(bal)) & 63u] = u.lane;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // see issue_batch
+            const int src = (int)(sh.stage[u.lane] << 2);
+            const uint32_t pk = ((__umul24((uint32_t)(y - u.yb), u.src.W) + (uint32_t)x) << 12) |
+                                (kd ? 0x100u : 0u) | c;
+            uint32_t nwv[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) nwv[m] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)w[m]);
+            const uint32_t npk = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pk);
+            if (u.lane >= q && u.lane < q + k) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) u.kq_w[m] = nwv[m];
+                u.kq_c = npk;
+            }
+            if (q + k >= 64u) {
+                score_kp_queue<N>(sh, u, 64u);
+                if (u.lane + 64u < q + k) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) u.kq_w[m] = nwv[m];
+                    u.kq_c = npk;
+                }
+            }
+            u.kq_n = (q + k) & 63u;
+        }
+        return;
+    }
+#endif
     if constexpr (NMS != kNmsOff) {
         // scores go to the band's LDS list, past its capacity to the band's slot (global),
         // past that they are only counted (the band NMS pass then recomputes all scores)
@@ -1083,6 +1161,9 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
 
     const uint32_t nunits = P.nstrips * P.nsub;
     const uint32_t sub_rows = (rows + P.nsub - 1) / P.nsub;
+#ifndef FDF_NO_KP_QUEUE
+    u.kq_n = 0;
+#endif
     // units are handed out dynamically: a wave that finishes early takes the next one
     // instead of idling at the workgroup barrier
     if (!(ablation_flags(P.flags) & kFlagNoPrefilter)) {
@@ -1113,6 +1194,11 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
                 sweep_unit<NMS, N, false>(sh, u, lk);
             }
         }
+#ifndef FDF_NO_KP_QUEUE
+        // the band's last keypoints: a partial queue (once per wave and band)
+        if constexpr (NMS == kNmsMaxThreshold)
+            if (u.kq_n != 0) score_kp_queue<N>(sh, u, u.kq_n);
+#endif
     }
     __syncthreads();
 
