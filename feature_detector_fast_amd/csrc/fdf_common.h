@@ -36,6 +36,27 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Division by a per-launch divisor d (a frame width, bitmap words per row) for x < 2^24:
+// q = hi32(x * m) with m = ceil(2^32 / d) is q_true or q_true + 1 (x * (m d - 2^32) / d
+// < x < 2^32 / 2^8), then one 24-bit multiply-compare corrects it -- 4 VALU instead of the
+// ~20 of a u32 division by a runtime value.  d = 1 has no 32-bit m (m = 0 marks it).
+// Converts to d, so `row * W` reads as before.
+struct RowDiv {
+    uint32_t d, m;
+    __device__ __forceinline__ operator uint32_t() const { return d; }
+};
+__device__ __forceinline__ RowDiv make_rowdiv(uint32_t d) {
+    RowDiv r;
+    r.d = d;
+    r.m = d >= 2u ? 0xffffffffu / d + 1u : 0u;
+    return r;
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t x, const RowDiv& r) {
+    if (r.m == 0u) return x;
+    const uint32_t q = __umulhi(x, r.m);
+    return q - (__umul24(q, r.d) > x ? 1u : 0u);
+}
+
 // Per-launch byte constants of the lerp comparisons (threshold t < 255).
 struct LerpConsts {
     uint32_t rb, kb, rd, kd;

@@ -65,19 +65,13 @@ __device__ __forceinline__ void compact_group(const CompactParams& P, uint32_t g
     const uint32_t cnt = mine ? P.counts[task] : 0u;
     const uint32_t slot_pts = P.slot_bytes / 8;
     const bool listed = cnt <= slot_pts;             // slot holds points (else its bitmap)
-    uint32_t total, list_total;
-    const uint32_t toff = block_exclusive_scan(cnt, sm.wave_sum, total);
-    const uint32_t loff = block_exclusive_scan(listed ? cnt : 0u, sm.wave_sum, list_total);
-    sm.task_off[tid] = toff;
-    sm.list_off[tid] = loff;
-    if (tid == 0) {
-        sm.task_off[kCompactTasks] = total;
-        sm.list_off[kCompactTasks] = list_total;
-    }
 
     // the group's base: every band count is final when this runs (the detector wrote them),
     // so each group sums its predecessors itself -- the per-group sums when the detector
-    // accumulated them, else the counts (16-byte loads, several in flight per thread)
+    // accumulated them, else the counts (16-byte loads, several in flight per thread).
+    // Loaded before the scans below: their barriers would otherwise order these loads
+    // after the counts' round trip (one memory latency more per group; a single frame's
+    // compaction is a chain of such latencies)
     unsigned long long part = 0;
     if (P.group_sums) {
         for (uint32_t i = tid; i < g; i += kCompactTasks) part += P.group_sums[i];
@@ -98,6 +92,16 @@ __device__ __forceinline__ void compact_group(const CompactParams& P, uint32_t g
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
     if (lane == 0) sm.part[wave] = part;
+
+    uint32_t total, list_total;
+    const uint32_t toff = block_exclusive_scan(cnt, sm.wave_sum, total);
+    const uint32_t loff = block_exclusive_scan(listed ? cnt : 0u, sm.wave_sum, list_total);
+    sm.task_off[tid] = toff;
+    sm.list_off[tid] = loff;
+    if (tid == 0) {
+        sm.task_off[kCompactTasks] = total;
+        sm.list_off[kCompactTasks] = list_total;
+    }
     __syncthreads();
     unsigned long long base = 0;
 #pragma unroll

@@ -369,14 +369,15 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x143, 0xc, 0xf, false));
             const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)e);
             const uint32_t sx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)excl);
-            {
-                const uint32_t bit = select_bit(se & 0xffffu, lane - sx);
-                // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column,
-                // kept in the lane (no LDS round trip: the lane reads only its own pixel)
-                scode = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
-            }
-            // the partial entry keeps the bits past the ones taken
-            if (has && excl < 64u && inc > 64u) m &= ~0u << select_bit(m, 64u - excl);
+            const uint32_t bit = select_bit(se & 0xffffu, lane - sx);
+            // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column,
+            // kept in the lane (no LDS round trip: the lane reads only its own pixel)
+            scode = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
+            // the partial entry keeps the bits past the ones taken: batch lane 63 took its
+            // last one (an entry is partial only when the batch is full), so one readlane
+            // replaces a second select
+            if (has && excl < 64u && inc > 64u)
+                m &= ~0u << (__builtin_amdgcn_readlane(bit, 63) + 1u);
 #endif
             // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
             const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
@@ -582,19 +583,53 @@ __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>:
 template <int NMS, int N, int LC>
 __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
                                             const LerpConsts& lk, bool (&inflight)[kSweepBatchSlots],
-                                            const Batch (&batch)[kSweepBatchSlots]) {
+                                            Batch (&batch)[kSweepBatchSlots]) {
+    constexpr int QL = kSweepBatchSlots - 1;
 #pragma unroll
-    for (int q = 0; q < kSweepBatchSlots; ++q) {
+    for (int q = 0; q < QL; ++q) {
         if (inflight[q]) {
             evaluate_batch<NMS, N, LC>(sh, u, lk, batch[q]);
             inflight[q] = false;
         }
     }
     if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;
-    while (u.tail != u.head) {
-        const Batch b = issue_batch<LC>(sh, u, true);
-        evaluate_batch<NMS, N, LC>(sh, u, lk, b);
+#ifndef FDF_PIPELINED_FLUSH_ALL
+    // max-t measured 0.6-1.0% slower with the pipelined flush (its keypoint queue and score
+    // keep more registers live), NMS off and SAD 0.2-1.5% faster (profiles/r02/ab_flush_rowdiv.txt)
+    constexpr bool serial = NMS == kNmsMaxThreshold;
+#else
+    constexpr bool serial = false;
+#endif
+    if constexpr (serial) {
+        if (inflight[QL]) evaluate_batch<NMS, N, LC>(sh, u, lk, batch[QL]);
+        inflight[QL] = false;
+        while (u.tail != u.head) {
+            const Batch b = issue_batch<LC>(sh, u, true);
+            evaluate_batch<NMS, N, LC>(sh, u, lk, b);
+        }
+        return;
     }
+    // Pipelined: the next batch's gathers are issued before the one in flight is evaluated,
+    // so a unit end with several queued batches waits for about one gather latency instead
+    // of one per batch (the order keypoints are found in does not matter: bitmap bits, and
+    // list entries ranked by position later).  Two batches alternate in fixed registers
+    // (A = the last slot, B), so no register with a load pending is ever copied.
+    Batch& A = batch[QL];
+    bool pa = inflight[QL];
+    while (u.tail != u.head) {
+        const Batch B = issue_batch<LC>(sh, u, true);
+        if (pa) evaluate_batch<NMS, N, LC>(sh, u, lk, A);
+        pa = false;
+        if (u.tail == u.head) {
+            evaluate_batch<NMS, N, LC>(sh, u, lk, B);
+            break;
+        }
+        A = issue_batch<LC>(sh, u, true);
+        pa = true;
+        evaluate_batch<NMS, N, LC>(sh, u, lk, B);
+    }
+    if (pa) evaluate_batch<NMS, N, LC>(sh, u, lk, A);
+    inflight[QL] = false;
 }
 
 template <int NMS, int N, bool EXACT>
@@ -860,10 +895,10 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
 // outside the band are reported as suppressed / not compared by the caller's rules below.
 // Returns e with its score field replaced by 1 (suppressed) or 0 (kept).
 __device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap, uint32_t nw,
-                                              uint32_t nb_blocks, uint32_t y0, uint32_t W,
+                                              uint32_t nb_blocks, uint32_t y0, RowDiv W,
                                               uint32_t H, const uint16_t* sranked,
                                               const uint16_t* bprefix, const uint32_t* rprefix) {
-    const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+    const uint32_t pos = e >> 12, row = udiv(pos, W), x = pos - row * W;
     const uint32_t y = y0 - 1 + row;
     const uint32_t own = e & 0xfffu;
     bool suppressed = y == 3 || y == H - 4;
@@ -914,11 +949,11 @@ __device__ __forceinline__ uint32_t keypoint_score_maxt(const __amdgpu_buffer_rs
 // without comparison, marked by a zero score.
 template <int NMS, int N>
 __device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitmap, uint32_t nw,
-                                                uint32_t R2, uint32_t nb_blocks, uint32_t W,
+                                                uint32_t R2, uint32_t nb_blocks, RowDiv W,
                                                 uint32_t y0, uint16_t* sranked,
                                                 const uint16_t* bprefix, const uint32_t* rprefix,
                                                 const __amdgpu_buffer_rsrc_t& frame) {
-    const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+    const uint32_t pos = e >> 12, row = udiv(pos, W), x = pos - row * W;
     if (neighbour_bits(bitmap, nw, R2, row, x) == 0) return e & ~0xfffu;
     if constexpr (NMS == kNmsMaxThreshold) {
         if (e & kScorePending)
@@ -928,15 +963,15 @@ __device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitm
     return e;
 }
 
-__device__ __forceinline__ void nms_clear(uint32_t e, uint32_t* bitmap, uint32_t nw, uint32_t W) {
+__device__ __forceinline__ void nms_clear(uint32_t e, uint32_t* bitmap, uint32_t nw, RowDiv W) {
     if ((e & 0xfffu) == 1u) {
-        const uint32_t pos = e >> 12, row = pos / W, x = pos - row * W;
+        const uint32_t pos = e >> 12, row = udiv(pos, W), x = pos - row * W;
         atomicAnd(&bitmap[row * nw + (x >> 5)], ~(1u << (x & 31)));
     }
 }
 
-__device__ __forceinline__ bool in_band_rows(uint32_t e, uint32_t W, uint32_t R2) {
-    const uint32_t row = (e >> 12) / W;
+__device__ __forceinline__ bool in_band_rows(uint32_t e, RowDiv W, uint32_t R2) {
+    const uint32_t row = udiv(e >> 12, W);
     return row != 0 && row != R2 - 1;                 // bitmap rows 0, R2-1: neighbours only
 }
 
@@ -951,7 +986,7 @@ __device__ __forceinline__ bool in_band_rows(uint32_t e, uint32_t W, uint32_t R2
 //   band's slot (`spill`); the LDS entries move to registers (kSpillPer per thread), so the
 //   ranked scores can use the whole FIFO + staging + list area.
 template <int NMS, int N>
-__device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+__device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, RowDiv W,
                              uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
                              uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags,
                              __amdgpu_buffer_rsrc_t frame) {
@@ -976,7 +1011,7 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
 constexpr uint32_t kSpillPer = kScoreListCap / kThreads;
 
 template <int NMS, int N>
-__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, uint32_t W,
+__device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, RowDiv W,
                                uint32_t H, const uint32_t* slist, uint32_t cap, uint32_t* spill,
                                uint32_t n, uint16_t* sranked, uint16_t* bprefix, uint32_t* rprefix,
                                uint32_t* total, __amdgpu_buffer_rsrc_t frame) {
@@ -1203,19 +1238,20 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     __syncthreads();
 
     const uint32_t nwords = rows * nw;
+    const RowDiv Wd = make_rowdiv(W), nwd = make_rowdiv(nw);
     if constexpr (NMS != kNmsOff) {
         const uint32_t n = *sh.slist_n;
         if (tid == 0 && P.kp_stats) atomicAdd(P.kp_stats, n);
         if (ablation_flags(P.flags) & kFlagNoNms) {
         } else if (n <= sh.slist_cap) {
-            band_nms_lds<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, n,
+            band_nms_lds<NMS, N>(bitmap, rows, nw, y0, Wd, H, sh.slist, n,
                                  reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                                  reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
                                  reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
                                  ablation_flags(P.flags), rs_exact);
         } else if (n - sh.slist_cap <= sh.spill_cap && n <= L.nms_area_entries) {
             // more keypoints than the LDS list holds: the rest were appended to the slot
-            band_nms_spill<NMS, N>(bitmap, rows, nw, y0, W, H, sh.slist, sh.slist_cap, sh.spill, n,
+            band_nms_spill<NMS, N>(bitmap, rows, nw, y0, Wd, H, sh.slist, sh.slist_cap, sh.spill, n,
                                    reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                                    reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
                                    reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
@@ -1263,7 +1299,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         uint32_t idx = before + incl - mine;
         for (uint32_t w = w_lo; w < w_hi; ++w) {
             uint32_t bits = keep[w];
-            const uint32_t r = w / nw;
+            const uint32_t r = udiv(w, nwd);
             const uint32_t xb = (w - r * nw) * 32;
             while (bits) {
                 const uint32_t bit = __builtin_ctz(bits);
@@ -1305,7 +1341,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
             const uint32_t inc = wave_incl_scan(c);
             uint32_t idx = o + inc - c;
             o += __builtin_amdgcn_readlane(inc, 63);
-            const uint32_t r = w / nw;
+            const uint32_t r = udiv(w, nwd);
             const uint32_t xb = (w - r * nw) * 32;
             while (bits) {
                 const uint32_t bit = __builtin_ctz(bits);
