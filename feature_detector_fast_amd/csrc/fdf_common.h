@@ -57,6 +57,11 @@ __device__ __forceinline__ uint32_t udiv(uint32_t x, const RowDiv& r) {
     return q - (__umul24(q, r.d) > x ? 1u : 0u);
 }
 
+// Byte 0 of x in all four bytes: one v_perm (x * 0x01010101 is a quarter-rate v_mul_lo_u32).
+__device__ __forceinline__ uint32_t bcast_byte(uint32_t x) {
+    return __builtin_amdgcn_perm(0u, x, 0u);
+}
+
 // Per-launch byte constants of the lerp comparisons (threshold t < 255).
 struct LerpConsts {
     uint32_t rb, kb, rd, kd;
@@ -105,7 +110,7 @@ template <int N>
 __device__ __forceinline__ void lane_segment_test_packed(uint32_t c, const uint32_t (&w)[4],
                                                          const LerpConsts& k, bool& bright,
                                                          bool& dark) {
-    const uint32_t nc = ~(c * 0x01010101u);
+    const uint32_t nc = ~bcast_byte(c);
     uint32_t fb[4], fn[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -231,7 +236,7 @@ __device__ __forceinline__ uint32_t score_sum_abs(uint32_t c, const uint32_t (&p
 __device__ __forceinline__ uint32_t score_sum_abs_packed(uint32_t c, const uint32_t (&w)[4],
                                                          uint32_t t) {
     const uint32_t U = min(c + t, 255u), L = c > t ? c - t : 0u;
-    const uint32_t U4 = U * 0x01010101u, L4 = L * 0x01010101u;
+    const uint32_t U4 = bcast_byte(U), L4 = bcast_byte(L);
     uint32_t su = 0, sl = 0, sp = 0;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {

@@ -442,11 +442,14 @@ __device__ __forceinline__ void append_scores(const SweepShared& sh, const UnitC
 template <int N>
 __device__ __forceinline__ void score_kp_queue(const SweepShared& sh, UnitCtx& u, uint32_t n) {
     const bool act = u.lane < n;
-    const uint32_t c = u.kq_c & 0xffu;
+    // dark keypoints score as bright ones on 255 - p: the packed words are inverted before
+    // they are unpacked (4 XORs instead of 16)
+    const uint32_t inv = (u.kq_c & 0x100u) ? ~0u : 0u;
+    const uint32_t c = (u.kq_c ^ inv) & 0xffu;
     uint32_t p[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = (u.kq_w[i & 3] >> (8 * (i >> 2))) & 0xffu;
-    const uint32_t score = score_max_threshold<N>(c, p, (u.kq_c >> 8) & 1u);
+    for (int i = 0; i < 16; ++i) p[i] = ((u.kq_w[i & 3] ^ inv) >> (8 * (i >> 2))) & 0xffu;
+    const uint32_t score = score_max_threshold<N>(c, p, false);
     append_scores(sh, u, act, n >= 64 ? ~0ull : (1ull << n) - 1ull,
                   (u.kq_c & 0xfffff000u) | score);
 }
@@ -483,7 +486,9 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
             if (is_kp) sh.stage[(q + lanes_below(bal)) & 63u] = u.lane;
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // see issue_batch
             const int src = (int)(sh.stage[u.lane] << 2);
-            const uint32_t pk = ((__umul24((uint32_t)(y - u.yb), u.src.W) + (uint32_t)x) << 12) |
+            // list position (bitmap row * W + x): masked operands make it a full-rate
+            // v_mul_u32_u24 (__umul24 here compiled to a quarter-rate v_mul_lo_u32)
+            const uint32_t pk = ((((uint32_t)(y - u.yb) & 0x3ffu) * (u.src.W & 0xffffffu) + (uint32_t)x) << 12) |
                                 (kd ? 0x100u : 0u) | c;
             uint32_t nwv[4];
 #pragma unroll
@@ -541,7 +546,7 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
                     score = score_sum_abs_packed(c, w, u.t);
                 }
                 const uint32_t idx = base + lanes_below(bal);
-                const uint32_t e = ((__umul24((uint32_t)(y - u.yb), u.src.W) + (uint32_t)x) << 12) | score;
+                const uint32_t e = ((((uint32_t)(y - u.yb) & 0x3ffu) * (u.src.W & 0xffffffu) + (uint32_t)x) << 12) | score;
                 if (idx < sh.slist_cap) sh.slist[idx] = e;
                 else if (idx - sh.slist_cap < sh.spill_cap) sh.spill[idx - sh.slist_cap] = e;
             }
@@ -1159,7 +1164,10 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.misc);
     if (P.threshold >= 255) return 0;                                // no pixel can pass
     uint32_t* unit_ctr = wave_sum + kWaves;
-    for (uint32_t i = tid; i <= (rows + 2 * halo) * nw; i += kThreads) bitmap[i] = 0;   // + pad
+    // the bitmap and its pad word, cleared 16 bytes per store up to the (16-byte aligned)
+    // end of its LDS area
+    for (uint32_t i = tid; i < L.pq / 16; i += kThreads)
+        reinterpret_cast<uint4*>(bitmap)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
         unit_ctr[0] = 0;
         unit_ctr[1] = 0;
