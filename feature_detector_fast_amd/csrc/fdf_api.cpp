@@ -230,7 +230,12 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     const uint32_t bands = (h - 6 + R - 1) / R;
     const uint64_t ntasks = (uint64_t)bands * n_frames;
     if (ntasks == 0 || ntasks > 0x7fffffffull) return FDF_ERR_SIZE;
-    const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw);
+    // A grid too small to fill the chip (a single frame) is latency-bound: its slots hold 4x
+    // the points (6% of the band's pixels instead of 1.6%), so that dense bands stay point
+    // lists and the compaction takes no bitmap expansion (a few hundred KB per frame)
+    // (fdf_ctx_set_geometry's forced full-size geometry keeps the full-size slots too)
+    const uint64_t fill = ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks;
+    const uint32_t slot_bytes = fdfk::slot_bytes_for(R, nw) * (ntasks < fill ? 4u : 1u);
     uint32_t tpg = fdfk::compact_tasks_per_group((uint32_t)ntasks);
     uint32_t flags = 0;
 #ifdef FDF_DEBUG_BUILD   // ablation builds only (libfdf_debug.so), see fdf_kernels.h
