@@ -81,6 +81,7 @@ constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix bl
 // band_nms_lds ranks the list's scores as u16 into the 4 candidate FIFOs
 static_assert(kScoreListCap * 2 <= 4 * kSweepPixelQ * 4, "ranked scores must fit the FIFO area");
 static_assert(kScoreListCap % 256 == 0, "the spill NMS pass holds the list 1/256 per thread");
+static_assert(kScoreListCap < 4096, "the LDS NMS pass keeps rank + 1 in a list entry's 12 score bits");
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
     uint32_t nms_area_entries;   // u16 ranked scores that fit [pq, bprefix) after the sweep

@@ -899,19 +899,25 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
 // neighbouring keypoints, read by raster rank from `sranked`; rows 3 / h-4 and the rows
 // outside the band are reported as suppressed / not compared by the caller's rules below.
 // Returns e with its score field replaced by 1 (suppressed) or 0 (kept).
+// RANKED (the LDS list, at most kScoreListCap entries): the scatter left the entry's raster
+// rank + 1 in its low 12 bits (its score is at that rank), so its own rank is not looked up
+// again.
+template <bool RANKED>
 __device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap, uint32_t nw,
                                               uint32_t nb_blocks, uint32_t y0, RowDiv W,
                                               uint32_t H, const uint16_t* sranked,
                                               const uint16_t* bprefix, const uint32_t* rprefix) {
     const uint32_t pos = e >> 12, row = udiv(pos, W), x = pos - row * W;
     const uint32_t y = y0 - 1 + row;
-    const uint32_t own = e & 0xfffu;
+    const uint32_t low = e & 0xfffu;
     bool suppressed = y == 3 || y == H - 4;
-    if (own != 0 && !suppressed) {
+    if (low != 0 && !suppressed) {
+        const uint32_t own = RANKED ? (uint32_t)sranked[low - 1u] : low;
         uint32_t mx = 0;
         const uint32_t mid = bits3(bitmap + row * nw, (int)x);
         if (mid & 5u) {
-            const uint32_t ro = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+            const uint32_t ro = RANKED ? low - 1u
+                                       : bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
             if (mid & 1u) mx = max(mx, (uint32_t)sranked[ro - 1]);
             if (mid & 4u) mx = max(mx, (uint32_t)sranked[ro + 1]);
         }
@@ -952,7 +958,7 @@ __device__ __forceinline__ uint32_t keypoint_score_maxt(const __amdgpu_buffer_rs
 // Rank-order scatter of list entry e: a keypoint with a neighbouring keypoint puts its score
 // at its raster rank (computing it first when it was deferred); an isolated one is kept
 // without comparison, marked by a zero score.
-template <int NMS, int N>
+template <int NMS, int N, bool RANKED = false>
 __device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitmap, uint32_t nw,
                                                 uint32_t R2, uint32_t nb_blocks, RowDiv W,
                                                 uint32_t y0, uint16_t* sranked,
@@ -964,7 +970,9 @@ __device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitm
         if (e & kScorePending)
             e = (e & ~0xfffu) | keypoint_score_maxt<N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), e & 1u);
     }
-    sranked[bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x)] = (uint16_t)(e & 0xfffu);
+    const uint32_t rank = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
+    sranked[rank] = (uint16_t)(e & 0xfffu);
+    if constexpr (RANKED) return (e & ~0xfffu) | (rank + 1u);
     return e;
 }
 
@@ -1000,13 +1008,13 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
     band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
     if (flags & kFlagNmsPrefixOnly) return;
     for (uint32_t i = tid; i < n; i += kThreads)
-        slist[i] = nms_scatter<NMS, N>(slist[i], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
-                                       rprefix, frame);
+        slist[i] = nms_scatter<NMS, N, true>(slist[i], bitmap, nw, R2, nb_blocks, W, y0, sranked,
+                                             bprefix, rprefix, frame);
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i];
         if (in_band_rows(e, W, R2))
-            slist[i] = nms_entry(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+            slist[i] = nms_entry<true>(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
     }
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) nms_clear(slist[i], bitmap, nw, W);
@@ -1037,11 +1045,11 @@ __device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j)
         if (in_band_rows(ent[j], W, R2))
-            ent[j] = nms_entry(ent[j], bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+            ent[j] = nms_entry<false>(ent[j], bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
     for (uint32_t i = tid; i < n - cap; i += kThreads) {
         const uint32_t e = spill[i];
         if (in_band_rows(e, W, R2))
-            spill[i] = nms_entry(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
+            spill[i] = nms_entry<false>(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
     }
     __syncthreads();
 #pragma unroll
