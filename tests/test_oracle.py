@@ -434,3 +434,46 @@ def test_max_threshold_packed_pairs():
             best = max(max(a, b) for a, b in MN)
             got = best - (c[i] if bright else 255 - c[i])
             assert got == oracle.score_max_threshold(int(c[i]), p.tolist(), n), (n, i)
+
+
+def test_rowdiv_multiply_high_division():
+    """fdf_common.h RowDiv / udiv: q = hi32(x * m) with m = 0xffffffff // d + 1 (= ceil(2^32 / d)),
+    then q -= (q * d > x), equals x // d for every x < 2^24 and d >= 2 (d = 1: m = 0 -> x).
+    Exhaustive over x < 4d + 10 for d < 5000 (all remainders), random x < 2^24 and large d."""
+    rng = np.random.default_rng(11)
+    divisors = list(range(1, 5000)) + rng.integers(5000, 1 << 20, 500).tolist() + [65535, 65536, 1 << 20]
+    for d in divisors:
+        x = np.concatenate([np.arange(0, min(1 << 24, 4 * d + 10), dtype=np.uint64),
+                            rng.integers(0, 1 << 24, 2000, dtype=np.uint64),
+                            np.array([(1 << 24) - 1], dtype=np.uint64)])
+        m = (0xffffffff // d + 1) if d >= 2 else 0
+        if m == 0:
+            q = x
+        else:
+            q = (x * np.uint64(m)) >> np.uint64(32)
+            q = q - ((q * np.uint64(d)) > x).astype(np.uint64)
+        assert np.array_equal(q, x // np.uint64(d)), d
+
+
+def test_byte_broadcast_and_partial_entry_mask():
+    """fdf_common.h bcast_byte (v_perm selector 0: byte 0 of the low source in all four bytes)
+    equals c * 0x01010101; the issue's partial FIFO entry keeps the bits above batch lane 63's
+    selected bit, which equals clearing below the (64 - excl)-th set bit (the old select)."""
+    for c in range(256):
+        perm = sum(c << (8 * k) for k in range(4))
+        assert perm == c * 0x01010101
+    rng = np.random.default_rng(12)
+
+    def select_bit(m, j):                 # position of the j-th set bit (fdf_sweep_impl.h)
+        return [b for b in range(16) if (m >> b) & 1][j]
+
+    for _ in range(20000):
+        m = int(rng.integers(1, 1 << 16))
+        k = bin(m).count("1")
+        taken = int(rng.integers(1, k)) if k > 1 else 0   # bits of the entry in this batch
+        if taken == 0:
+            continue
+        last = select_bit(m, taken - 1)                    # batch lane 63's bit
+        new = m & ((~0 << (last + 1)) & 0xffffffff)
+        old = m & ((~0 << select_bit(m, taken)) & 0xffffffff)
+        assert new == old
