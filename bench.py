@@ -48,6 +48,10 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="budget for the single-thread CPU baseline sample (0 = skip)")
     p.add_argument("--no-extras", action="store_true", help="skip latency/parity extras")
+    p.add_argument("--input", default=os.environ.get("INPUT_FILE", ""),
+                   help="an image (PNG/PGM, converted as image 0.24.6 to_luma8) for the "
+                        "single-frame GPU and CPU legs, as the reference's bench takes "
+                        "INPUT_FILE (benches/benchmark.rs:6-7); the batch stays synthetic")
     return p.parse_args(argv)
 
 
@@ -138,68 +142,141 @@ def barrier(world):
 
 
 def load_traffic(cfg_key):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if one matches."""
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/
+    pmc_traffic.json), and the entry's stamp: (bytes, {"src_sha16", "rev", "stale"}).  An
+    entry profiled from other kernel sources than the ones in this tree is stale: its bytes
+    are not reported (None) and the stamp says so."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            data = json.load(f)
-        return data.get(cfg_key, {}).get("hbm_bytes_per_launch")
+            entry = json.load(f).get(cfg_key, {})
     except (OSError, ValueError):
-        return None
+        entry = {}
+    if not entry:
+        return None, None
+    import workloads
+    now = workloads.kernel_source_sha16()
+    stamp = {"src_sha16": entry.get("src_sha16"), "rev": entry.get("rev"),
+             "stale": entry.get("src_sha16") != now}
+    return (None if stamp["stale"] else entry.get("hbm_bytes_per_launch")), stamp
+
+def gpu_clocks(device_index):
+    """The GPU's current sclk / mclk and package power from rocm-smi (None fields when it
+    is missing): taken while the detector runs back to back (see clock_probe)."""
+    import subprocess
+    res = {"sclk_mhz": None, "mclk_mhz": None, "power_w": None}
+    try:
+        out = subprocess.run(["rocm-smi", "-d", str(device_index), "--showclocks", "--showpower",
+                              "--json"], capture_output=True, text=True, timeout=20).stdout
+        card = next(iter(json.loads(out).values()))
+    except Exception:                       # noqa: BLE001 -- a missing tool is not an error
+        return res
+    def mhz(v):
+        try:
+            return float(str(v).strip("()").lower().replace("mhz", "").split()[0])
+        except (ValueError, IndexError):
+            return None
+    for k, v in card.items():
+        kl = k.lower()
+        if "sclk" in kl and "clock" in kl and res["sclk_mhz"] is None:
+            res["sclk_mhz"] = mhz(v)
+        elif "mclk" in kl and "clock" in kl and res["mclk_mhz"] is None:
+            res["mclk_mhz"] = mhz(v)
+        elif "power" in kl and res["power_w"] is None:
+            try:
+                res["power_w"] = float(str(v).split()[0])
+            except ValueError:
+                pass
+    return res
 
 
-def cpu_baseline(args, nms):
+def clock_probe(fast_hip, copies, cfg, out, offs, stream, device, seconds=2.0):
+    """rocm-smi's clocks and power sampled halfway through ~`seconds` of back-to-back
+    detector launches (the bench's own workload), from a helper thread."""
+    import threading
+
+    import torch
+
+    sample = {}
+    stop = threading.Event()
+
+    def probe():
+        stop.wait(seconds / 2)
+        sample.update(gpu_clocks(device.index or 0))
+
+    th = threading.Thread(target=probe)
+    t0 = time.perf_counter()
+    th.start()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(10):
+            fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+            k += 1
+        torch.cuda.synchronize()
+    th.join()
+    idle = gpu_clocks(device.index or 0)
+    return {"under_load": sample, "after": idle, "launches": k}
+
+
+def cpu_baseline(args, nms, single_img=None):
     """The AVX2 port of the reference path (oracle/fast_avx2.cpp) on the host cores, rank 0,
     N=1 (benches/benchmark.rs:18-50 protocol):
       * single frame, 1 thread: NMS off / max-t / SAD, 10 warm-up calls then 100 timed calls
-        each, median and its 95% CI (config 1 is the off leg);
+        each, median and its 95% CI (config 1 is the off leg), on `single_img` (--input)
+        or one S1 frame;
       * throughput, 1 thread (the headline `cpu_baseline`): 8 S1 frames x N repetitions in
         the bench's NMS mode, ~args.cpu_seconds of CPU work;
-      * all cores: one frame per thread over the same sample with nproc threads (and with
-        the box's CPU share), CPU model, nproc and cgroup quota stated."""
+      * all cores: the bench's whole S1 batch (args.frames frames), one
+        frame at a time per thread, with min(CPUs this process may use, cgroup CPU quota)
+        threads, each pinned to its own CPU -- no more threads than the quota runs at once."""
     import workloads
     from oracle import oracle
 
     W, H = args.width, args.height
-    frame = workloads.s1_frame(0, W, H)
+    frame = workloads.s1_frame(0, W, H) if single_img is None else single_img
+    fh, fw = frame.shape
     single = {}
     for name, mode in (("off", 0), ("maxt", 1), ("sad", 2)):
         ms, kp = oracle.avx2_samples(frame, args.threshold, args.count, mode, 10, 100)
         med, ci = median_ci95(ms)
         single[name] = {"ms_median": round(med, 4), "ms_ci95": [round(ci[0], 4), round(ci[1], 4)],
-                        "Mpix_s": round(W * H / (med * 1e-3) / 1e6, 1), "keypoints": kp,
+                        "Mpix_s": round(fw * fh / (med * 1e-3) / 1e6, 1), "keypoints": kp,
                         "warmup": 10, "samples": 100}
     frames = np.stack([workloads.s1_frame(i, W, H) for i in range(8)])
     secs1, _ = oracle.avx2_time(frames[:1], args.threshold, args.count, nms, 1, 1)
     reps = max(1, int(args.cpu_seconds / max(secs1, 1e-6) / len(frames)))
     secs, kp = oracle.avx2_time(frames, args.threshold, args.count, nms, 1, reps)
     px = float(W * H) * len(frames) * reps
+    nproc = os.cpu_count() or 1
     base = {"value": round(px / secs / 1e6, 1), "unit": "Mpixels/s", "cores": 1, "kind": "port",
             "sample": f"{len(frames)} S1 {W}x{H} frames x {reps} reps, "
                       f"t={args.threshold} n={args.count} nms={args.nms}, 1 thread, "
                       f"AVX2 port of src/fast_simd.rs (oracle/fast_avx2.cpp), {secs:.1f} s",
             "ms_per_frame": round(secs * 1e3 / (len(frames) * reps), 4),
-            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "cpu": cpu_model(), "nproc": nproc,
+            "single_frame_image": args.input or "S1 frame 0",
             "single_frame": single}
-    nproc = os.cpu_count() or 1
     try:
-        share = len(os.sched_getaffinity(0))
+        allowed = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        share = nproc
+        allowed = list(range(nproc))
     quota = cpu_quota()
-    legs = {}
-    for label, threads in (("nproc", nproc), ("affinity", share)):
-        if label == "affinity" and threads == nproc:
-            continue
-        # ~3 s of work spread over the threads, at least 2 frames per thread
-        reps_mt = max(1, int(3.0 * min(threads, quota or threads) / max(secs1, 1e-6) / len(frames)),
-                      2 * threads // len(frames))
-        secs_mt, _ = oracle.avx2_time(frames, args.threshold, args.count, nms, threads, reps_mt)
-        legs[label] = {"value": round(px / reps * reps_mt / secs_mt / 1e6, 1),
-                       "unit": "Mpixels/s", "threads": threads, "seconds": round(secs_mt, 2),
-                       "frames": len(frames) * reps_mt}
-    mt = {"kind": "port", "cpu": cpu_model(), "nproc": nproc, "affinity_cpus": share,
-          "cgroup_cpu_quota": quota, "nms": args.nms, **legs}
+    threads = max(1, min(len(allowed), int(quota) if quota else len(allowed)))
+    cpus = allowed[:threads]
+    nb = max(1, args.frames)
+    batch = np.stack([workloads.s1_frame(i, W, H) for i in range(nb)])
+    per_pass = secs1 * nb / threads
+    reps_mt = max(1, int(3.0 / max(per_pass, 1e-6)))
+    secs_mt, _ = oracle.avx2_time(batch, args.threshold, args.count, nms, threads, reps_mt,
+                                  cpus=cpus)
+    del batch
+    mt = {"kind": "port", "cpu": cpu_model(), "nproc": nproc, "affinity_cpus": len(allowed),
+          "cgroup_cpu_quota": quota, "threads": threads, "pinned": True,
+          "cpus": [cpus[0], cpus[-1]], "nms": args.nms,
+          "sample": f"{nb} S1 {W}x{H} frames x {reps_mt} passes, frame f on thread f % {threads}, "
+                    f"thread i pinned to CPU cpus[i] (sched_setaffinity)",
+          "value": round(float(W * H) * nb * reps_mt / secs_mt / 1e6, 1), "unit": "Mpixels/s",
+          "seconds": round(secs_mt, 2)}
     return base, mt
 
 
@@ -354,6 +431,28 @@ def rgb_path(fast_hip, cfg, frames, out, offs, stream, nframes=256, steps=10):
     return res
 
 
+def input_file_checks(fast_hip, Config, NonMaximalSuppression, workloads, oracle, path, grey,
+                      rgb):
+    """tests/compare.rs on --input: the five configurations, GPU against the CPU oracle (keypoint
+    counts stated, so the README's 23 184 / 7 646 / 8 307 can be checked on its image), and the
+    reference's hash guard (compare.rs:83-89: if the RGB bytes hash to its test image's hash,
+    the max-t keypoints must hash to 0x8bf9cd0f9ca9ebec)."""
+    res = {"path": path, "width": int(grey.shape[1]), "height": int(grey.shape[0]), "configs": {}}
+    for name, t, n, m in (("non_max_suppression_t16_c_9", 16, 9, 0), ("max_threshold_t16_c_9", 16, 9, 1),
+                          ("sum_absolute_t16_c_9", 16, 9, 2), ("sum_absolute_t16_c_12", 16, 12, 2),
+                          ("sum_absolute_t32_c_16", 32, 12, 2)):
+        got = fast_hip.detect_array(grey, Config(t, n, NonMaximalSuppression(m)))
+        want = oracle.detect(grey, t, n, m)
+        res["configs"][name] = {"keypoints": int(len(got)), "bit_exact": bool(np.array_equal(got, want))}
+        if m == 1:
+            h = workloads.rust_hash_points(got)
+            img_h = workloads.rust_hash_bytes(rgb)
+            res["hash_keypoints"] = f"0x{h:x}"
+            res["reference_test_image"] = img_h == workloads.REF_IMAGE_HASH
+            res["hash_guard_ok"] = img_h != workloads.REF_IMAGE_HASH or h == workloads.REF_MAXT_HASH
+    return res
+
+
 def make_batch(workloads, first, count, W, H, device, min_bytes=0):
     """`count` S1 frames from global index `first`, plus identical copies until the copies
     together hold >= min_bytes: a step reads copy k % len(copies), so a shard smaller than
@@ -392,12 +491,15 @@ def timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, steps, warmup, wo
 
 
 def roofline_of(det_ms, com_ms, alg_bytes, call_bytes, traffic):
-    """Roofline of the detector kernel from its per-launch HIP-event durations."""
+    """Roofline of the detector kernel from its per-launch HIP-event durations; `traffic`
+    is load_traffic()'s (bytes, stamp)."""
     sweep = float(np.mean(det_ms)) if len(det_ms) else float("nan")
     comp = float(np.mean(com_ms)) if len(com_ms) else float("nan")
     achieved = alg_bytes / (sweep * 1e-3) / 1e9
+    tbytes, tstamp = traffic
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tbytes,
+            "traffic_stamp": tstamp,
             "kernel": "fast_sweep_kernel", "kernel_ms_avg": round(sweep, 4),
             "kernel_ms": percentiles(det_ms), "timed_launches": int(len(det_ms)),
             "alg_bytes_per_launch": int(alg_bytes),
@@ -486,24 +588,27 @@ def main(argv=None):
     extras = {}
     cpu = None
     if not args.no_extras:
-        # the other half of the headline metric ("with and without NMS"): the same batch,
-        # NMS off (or max-t when the headline is off), same protocol
-        other = "off" if nms != 0 else "maxt"
-        ocfg = Config(args.threshold, args.count, NonMaximalSuppression(NMS_NAMES[other]))
-        e2, d2, c2 = timed_steps(fast_hip, ctx, copies, ocfg, out, offs, stream, args.steps,
-                                 args.warmup, world)
-        e2 = reduce_max(e2, world, device)
-        kp2 = int(offs[-1].item())
-        pts2 = out[: min(kp2, cap)].cpu().numpy().astype(np.uint32)
-        leg = {"workload": f"same batch, nms={other}",
-               "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
-               "ms_per_step": round(e2 * 1e3 / args.steps, 4),
-               "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
-               "roofline": roofline_of(d2, c2, alg_bytes, alg_bytes + 8 * kp2 + 8 * (count + 1),
-                                       load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
-               "parity": check_parity(oracle, frames, pts2, offs.cpu().numpy(), first, count,
-                                      args.threshold, args.count, NMS_NAMES[other], W)}
-        extras[f"nms_{other}"] = leg
+        # the GPU's clocks and power while this workload runs back to back (rocm-smi), so a
+        # box-to-box difference in kernel time can be told apart from a clock difference
+        extras["gpu_clock"] = clock_probe(fast_hip, copies, cfg, out, offs, stream, device)
+        # the other NMS modes on the same batch, same protocol: the headline metric is "with
+        # and without NMS", and the reference's bench times all three (benches/benchmark.rs:18-50)
+        for other in [m for m in ("off", "maxt", "sad") if m != args.nms]:
+            ocfg = Config(args.threshold, args.count, NonMaximalSuppression(NMS_NAMES[other]))
+            e2, d2, c2 = timed_steps(fast_hip, ctx, copies, ocfg, out, offs, stream, args.steps,
+                                     args.warmup, world)
+            e2 = reduce_max(e2, world, device)
+            kp2 = int(offs[-1].item())
+            pts2 = out[: min(kp2, cap)].cpu().numpy().astype(np.uint32)
+            leg = {"workload": f"same batch, nms={other}",
+                   "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
+                   "ms_per_step": round(e2 * 1e3 / args.steps, 4),
+                   "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
+                   "roofline": roofline_of(d2, c2, alg_bytes, alg_bytes + 8 * kp2 + 8 * (count + 1),
+                                           load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
+                   "parity": check_parity(oracle, frames, pts2, offs.cpu().numpy(), first, count,
+                                          args.threshold, args.count, NMS_NAMES[other], W)}
+            extras[f"nms_{other}"] = leg
         if world > 1 and not strong:
             # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU
             f4, c4 = strong_shard(rank, world, 512)
@@ -520,8 +625,19 @@ def main(argv=None):
                 "kernel_ms": percentiles(d4)}
             del cop4
     if rank == 0 and not args.no_extras:
-        # single-frame latency (device-resident frame, one launch, HIP events)
-        one = frames[:1].contiguous()
+        # single-frame latency (device-resident frame, one launch, HIP events), on --input
+        # when given (the reference's bench image, benches/benchmark.rs:6-16), else S1 frame 0
+        single_img = None
+        if args.input:
+            import workloads
+            single_img, rgb_in = workloads.input_image(args.input)
+            extras["input_file"] = input_file_checks(fast_hip, Config, NonMaximalSuppression,
+                                                     workloads, oracle, args.input, single_img,
+                                                     rgb_in)
+            one = torch.from_numpy(single_img).to(device).unsqueeze(0).contiguous()
+        else:
+            one = frames[:1].contiguous()
+        oh, ow = one.shape[1], one.shape[2]
         for name, mode in (("off", 0), ("maxt", 1)):
             c1 = Config(args.threshold, args.count, NonMaximalSuppression(mode))
             for _ in range(10):
@@ -536,9 +652,9 @@ def main(argv=None):
             torch.cuda.synchronize()
             lat = sorted(s.elapsed_time(e) for s, e in ev)
             extras[f"single_frame_{name}_ms_p50"] = round(lat[len(lat) // 2], 4)
-            extras[f"single_frame_{name}_Mpix_s"] = round(W * H / (lat[len(lat) // 2] * 1e-3) / 1e6, 1)
+            extras[f"single_frame_{name}_Mpix_s"] = round(ow * oh / (lat[len(lat) // 2] * 1e-3) / 1e6, 1)
             extras[f"single_frame_{name}_kp"] = int(offs[1].item())
-        host = frames[0].cpu().numpy()
+        host = one[0].cpu().numpy()
         extras["host_fdf_detect_ms"] = host_latency(
             fast_hip, _native, host,
             {"off": (cfg, 0), "maxt": (cfg, 1)})
@@ -546,7 +662,7 @@ def main(argv=None):
                                           out, stream, device, oracle.detect)
         extras["rgb_path"] = rgb_path(fast_hip, cfg, frames, out, offs, stream)
         if world == 1 and args.cpu_seconds > 0:
-            cpu, cpu_mt = cpu_baseline(args, nms)
+            cpu, cpu_mt = cpu_baseline(args, nms, single_img)
             extras["cpu_baseline_all_cores"] = cpu_mt
             sf = cpu["single_frame"]
             extras["gpu_vs_cpu_single_frame"] = {

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "fdf_pipeline_collect", "fdf_ctx_set_geometry", "fdf_ctx_timing_samples", "fdf_fetch_last",
     "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
     "fdf_detect_device_rgb", "fdf_circle", "fdf_calculate_offsets", "fdf_score_rings",
-    "fdf_score_rings_device",
+    "fdf_score_rings_device", "fdf_ctx_set_band_rows",
 )
 
 
@@ -161,6 +161,8 @@ def load():
     lib.fdf_ctx_workspace_bytes.argtypes = [vp, ctypes.POINTER(u64)]
     lib.fdf_ctx_set_geometry.restype = ctypes.c_int
     lib.fdf_ctx_set_geometry.argtypes = [vp, u32]
+    lib.fdf_ctx_set_band_rows.restype = ctypes.c_int
+    lib.fdf_ctx_set_band_rows.argtypes = [vp, u32]
     lib.fdf_ctx_timing_samples.restype = ctypes.c_int
     lib.fdf_ctx_timing_samples.argtypes = [vp, vp, vp, u32, ctypes.POINTER(u32)]
     lib.fdf_fetch_last.restype = ctypes.c_int
@@ -233,6 +235,11 @@ class Context:
         """Band geometry override (fdf_ctx_set_geometry): min_tasks=1 gives small jobs the
         tall bands of large batches (tests); 0 restores the default."""
         check(self._lib.fdf_ctx_set_geometry(self.handle, int(min_tasks)))
+
+    def set_band_rows(self, rows=0):
+        """Band height override (fdf_ctx_set_band_rows): bands of ``rows`` centre rows for
+        every later detection (same keypoints, other NMS tiers); 0 = automatic."""
+        check(self._lib.fdf_ctx_set_band_rows(self.handle, int(rows)))
 
     def close(self):
         if self.handle:

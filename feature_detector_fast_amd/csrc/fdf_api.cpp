@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -27,6 +28,10 @@ struct LastResult {
     uint32_t n_frames = 0, width = 0, height = 0;
     fdf_config cfg{};
     bool rgb = false;              // frames in d_rgb (RGB8); scores need their luma in d_in
+    // fdf_detect_batch_multi: the call's generation (0: not a multi-context result) and this
+    // context's shard of it, checked by fdf_fetch_last_multi
+    uint64_t multi_gen = 0;
+    uint32_t shard = 0, nshards = 0;
 };
 
 struct fdf_ctx {
@@ -42,8 +47,8 @@ struct fdf_ctx {
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
     // compaction bases: two alternating buffers of per-group sums (kept zero between uses)
-    // and the fused-compaction ticket, all zeroed once at context creation
-    uint32_t* d_sums = nullptr;         // 2 x fdfk::kMaxGroupSums, then the ticket
+    // and the keypoint-statistics word, all zeroed once at context creation
+    uint32_t* d_sums = nullptr;         // 2 x fdfk::kMaxGroupSums, then 4 words
     int sums_parity = 0;
     bool sums_dirty = false;            // a launch failed: re-zero before the next use
     // NMS keypoint density feedback (band height): the compaction writes the last finished
@@ -63,10 +68,14 @@ struct fdf_ctx {
     LastResult last;
     // grid size that counts as filling the chip (fdf_ctx_set_geometry; 0 = kDefaultMinTasks)
     uint64_t min_tasks = 0;
+    uint32_t band_rows = 0;              // fdf_ctx_set_band_rows (0 = automatic)
     // optional per-kernel timing (fdf_ctx_set_timing): 3 events around each call's launches
     bool timing = false;
     size_t timed = 0;                     // calls recorded since timing was enabled
     std::vector<hipEvent_t> ev;           // 3 per recorded call, kMaxTimedCalls at most
+    // debug builds (FDF_STAMPS set): the last detector launch's workgroup stamps
+    uint64_t* d_stamps = nullptr;         size_t stamps_n = 0;
+    uint64_t stamps_used = 0;             // words written by the last launch
 };
 
 constexpr size_t kMaxTimedCalls = 4096;
@@ -138,7 +147,7 @@ struct Geometry {
 
 
 Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
-                       uint64_t min_tasks, double density) {
+                       uint64_t min_tasks, double density, uint32_t forced_rows) {
     Geometry g;
     const uint32_t sc = (uint32_t)fdfk::strip_cols(fdfk::kLaneCols);
     g.nstrips = (w - 3 + sc - 1) / sc;
@@ -172,6 +181,12 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     if (nms && density > 0.0) {
         const double rows = (double)fdfk::kScoreListCap / (1.5 * density * (double)w) - 2.0;
         max_rows = rows < (double)g.nsub ? g.nsub : (rows > 256.0 ? 256u : (uint32_t)rows);
+    }
+    if (forced_rows) {   // fdf_ctx_set_band_rows: the height asked for, as far as LDS allows
+        g.R = (forced_rows + g.nsub - 1) / g.nsub * g.nsub;
+        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, nms).total > fdfk::kSweepMaxLds)
+            g.R -= g.nsub;
+        return g;
     }
     double best = -1.0;
     g.R = 0;
@@ -222,7 +237,8 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         }
     }
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms,
-                                       ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks, density);
+                                       ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks, density,
+                                       ctx->band_rows);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
     if (fdfk::make_sweep_layout(R, nw, cfg->nms).total > fdfk::kSweepMaxLds)
@@ -268,17 +284,11 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
             return FDF_ERR_DEVICE;
         ctx->sums_dirty = false;
     }
-    // fused compaction (the detector's last workgroup orders the bands) is built but off:
-    // every workgroup's device-scope release is an L2 writeback on gfx950 (buffer_wbl2 sc1),
-    // and one frame measured 87 us fused against 10 + 9 us as two launches
-#ifdef FDF_FUSED_COMPACT
-    const bool fused = ntasks <= fdfk::kFusedCompactTasks;
-#else
-    const bool fused = false;
-#endif
-    if (fused) tpg = (uint32_t)ntasks;                  // one group, run by the last band
+    // detection and compaction are two launches: a compaction fused into the detector's last
+    // workgroup measured 87 us for one frame against 13 + 12 us (every workgroup's device-scope
+    // release is an L2 writeback on gfx950)
     const uint64_t ngroups = (ntasks + tpg - 1) / tpg;
-    const bool grouped = !fused && ngroups <= fdfk::kMaxGroupSums;
+    const bool grouped = ngroups <= fdfk::kMaxGroupSums;
     uint32_t* sums_now = ctx->d_sums + (size_t)ctx->sums_parity * fdfk::kMaxGroupSums;
     uint32_t* sums_next = ctx->d_sums + (size_t)(1 - ctx->sums_parity) * fdfk::kMaxGroupSums;
     fdfk::BandParams p;
@@ -315,8 +325,16 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.next_sums = sums_next;
     p.group_sums = grouped ? sums_now : nullptr;
     p.tasks_per_group = tpg;
-    p.ticket = ctx->d_sums + 2 * fdfk::kMaxGroupSums;
     p.kp_stats = nullptr;
+    p.stamps = nullptr;
+#ifdef FDF_DEBUG_BUILD
+    if (std::getenv("FDF_STAMPS")) {
+        const size_t words = (size_t)ntasks * fdfk::kStampWords;
+        if ((rc = ensure(ctx, &ctx->d_stamps, &ctx->stamps_n, words, stream))) return rc;
+        p.stamps = ctx->d_stamps;
+        ctx->stamps_used = words;
+    }
+#endif
     c.kp_stats = nullptr;
     c.stats_out = nullptr;
     c.stats_seq = 0;
@@ -334,8 +352,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         c.stats_out = ctx->d_stats;
         c.stats_seq = seq;
     }
-    p.fused = fused ? 1u : 0u;
-    p.compact = c;
     hipEvent_t* ev = nullptr;
     if (ctx->timing && ctx->timed < kMaxTimedCalls) {
         while (ctx->ev.size() < 3 * (ctx->timed + 1)) {
@@ -352,8 +368,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         return FDF_ERR_DEVICE;
     }
     if (ev && hipEventRecord(ev[1], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    // small grids compacted inside the detector launch (its last workgroup)
-    if (!fused && fdfk::launch_compact(c, stream) != hipSuccess) {
+    if (fdfk::launch_compact(c, stream) != hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
@@ -534,6 +549,19 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
     return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
 
+// Locks the contexts of a multi-context call in one global order (by address), whatever
+// order the caller lists them in: two calls over the same contexts cannot deadlock.
+std::vector<std::unique_lock<std::mutex>> lock_all(fdf_ctx* const* ctxs, uint32_t n) {
+    std::vector<fdf_ctx*> order(ctxs, ctxs + n);
+    std::sort(order.begin(), order.end(), std::less<fdf_ctx*>());
+    std::vector<std::unique_lock<std::mutex>> locks;
+    locks.reserve(n);
+    for (fdf_ctx* c : order) locks.emplace_back(c->mu);
+    return locks;
+}
+
+std::atomic<uint64_t> g_multi_gen{0};
+
 // Copy of the last host result (fdf_fetch_last), lock held.
 int fetch_last(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t cap, size_t* n_out) {
     if (!ctx->last.valid) return FDF_ERR_ARG;
@@ -611,6 +639,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_sums);
+        (void)hipFree(ctx->d_stamps);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         if (ctx->done) (void)hipEventDestroy(ctx->done);
         if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
@@ -643,6 +672,13 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
     if (!ctx) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->min_tasks = min_tasks;
+    return FDF_OK;
+}
+
+int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows) {
+    if (!ctx) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->band_rows = rows;
     return FDF_OK;
 }
 
@@ -956,13 +992,19 @@ int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* 
     int rc = check_host_args(data, n_frames, width, height, width, cfg, false, &empty);
     if (rc) return rc;
     std::vector<uint64_t> offs(n_frames + 1ull, 0);
-    std::vector<std::unique_lock<std::mutex>> locks;
-    for (uint32_t k = 0; k < n_ctx; ++k) locks.emplace_back(ctxs[k]->mu);   // held throughout
+    const auto locks = lock_all(ctxs, n_ctx);                     // held throughout
+    const uint64_t gen = ++g_multi_gen;
+    auto tag = [&](uint32_t k) {
+        ctxs[k]->last.multi_gen = gen;
+        ctxs[k]->last.shard = k;
+        ctxs[k]->last.nshards = n_ctx;
+    };
     if (empty) {
         for (uint32_t k = 0; k < n_ctx; ++k) {
             ctxs[k]->last = LastResult{};
             ctxs[k]->last.valid = true;
             ctxs[k]->last.cfg = *cfg;
+            tag(k);
         }
         *n_out = 0;
         if (frame_offsets) std::memset(frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull));
@@ -996,6 +1038,7 @@ int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* 
     run_all(detect_shard);
     for (uint32_t k = 0; k < n_ctx; ++k)
         if (status[k]) return status[k];
+    for (uint32_t k = 0; k < n_ctx; ++k) tag(k);
     // global offsets: shard k's points follow shards 0 .. k-1
     std::vector<uint64_t> base(n_ctx + 1, 0);
     for (uint32_t k = 0; k < n_ctx; ++k) {
@@ -1022,13 +1065,19 @@ int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* 
 int fdf_fetch_last_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, fdf_point* out, size_t cap,
                          size_t* n_out) {
     if (!ctxs || n_ctx == 0 || n_ctx > 1024 || !n_out || (cap && !out)) return FDF_ERR_ARG;
-    std::vector<std::unique_lock<std::mutex>> locks;
     for (uint32_t k = 0; k < n_ctx; ++k) {
         if (!ctxs[k]) return FDF_ERR_ARG;
         for (uint32_t j = 0; j < k; ++j)
             if (ctxs[j] == ctxs[k]) return FDF_ERR_ARG;
-        locks.emplace_back(ctxs[k]->mu);
-        if (!ctxs[k]->last.valid) return FDF_ERR_ARG;
+    }
+    const auto locks = lock_all(ctxs, n_ctx);
+    // the results must be the shards of ONE fdf_detect_batch_multi call, in its order (a
+    // host call on one of the contexts since then, or a reordered array, is an error)
+    const uint64_t gen = ctxs[0]->last.multi_gen;
+    for (uint32_t k = 0; k < n_ctx; ++k) {
+        const LastResult& L = ctxs[k]->last;
+        if (!L.valid || gen == 0 || L.multi_gen != gen || L.shard != k || L.nshards != n_ctx)
+            return FDF_ERR_ARG;
     }
     uint64_t b = 0;
     for (uint32_t k = 0; k < n_ctx; ++k) {
@@ -1044,5 +1093,22 @@ int fdf_fetch_last_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, fdf_point* out, s
     *n_out = (size_t)b;
     return b > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
+
+#ifdef FDF_DEBUG_BUILD
+// Debug builds only (not in include/fdf.h): the last detector launch's workgroup stamps,
+// fdfk::kStampWords words per workgroup in blockIdx order (tools/stamps.py).
+int fdf_debug_stamps(fdf_ctx* ctx, uint64_t* out, uint64_t cap_words, uint64_t* n_words) {
+    if (!ctx || !n_words) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    DeviceGuard guard(ctx->device);
+    *n_words = ctx->stamps_used;
+    if (!ctx->d_stamps || !out) return FDF_OK;
+    wait_done(ctx);
+    const size_t n = (size_t)std::min<uint64_t>(cap_words, ctx->stamps_used);
+    return hipMemcpy(out, ctx->d_stamps, n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess
+               ? FDF_OK
+               : FDF_ERR_DEVICE;
+}
+#endif
 
 }  // extern "C"

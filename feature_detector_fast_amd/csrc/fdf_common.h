@@ -65,7 +65,6 @@ __device__ __forceinline__ uint32_t bcast_byte(uint32_t x) {
 // Per-launch byte constants of the lerp comparisons (threshold t < 255).
 struct LerpConsts {
     uint32_t rb, kb, rd, kd;
-    uint32_t kb0, kd0;   // pre-filter (rounding 0 for both polarities), see prefilter_compare
 };
 __device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
     LerpConsts k;
@@ -74,12 +73,6 @@ __device__ __forceinline__ LerpConsts lerp_consts(uint32_t t) {
     k.kb = (128u - ((t + ob) >> 1)) * 0x01010101u;
     k.rd = od * 0x01010101u;
     k.kd = (255u - ((254u - t + od) >> 1)) * 0x01010101u;
-    // With D = x - c + 255 and v = lerp(x, ~c, 0) = D >> 1, bit 7 of lerp(v, 256 - k, 0) is
-    // D >= 2k.  Bright is D >= t + 256 and not-dark is D >= 255 - t; the threshold of the
-    // odd one is rounded so that bright flags only gain pixels and not-dark flags only lose
-    // them, i.e. the pre-filter only gains candidates: k = (t + 256) / 2, (256 - t) / 2.
-    k.kb0 = (256u - ((t + 256u) >> 1)) * 0x01010101u;
-    k.kd0 = (256u - ((256u - t) >> 1)) * 0x01010101u;
     return k;
 }
 
@@ -155,63 +148,6 @@ __device__ __forceinline__ uint32_t score_max_threshold(uint32_t c, const uint32
         best = max(best, min(min(m6[i], m6[(i + K) & 15]), m6[(i + N - 6) & 15]));
     }
     return best - (c ^ m);
-}
-
-// The same max-threshold score from the packed ring (byte j of w[m] = circle pixel 4j + m),
-// over u16 pairs: register k holds the values of the windows starting at 2k and 2k + 1, so
-// every v_pk_min_u16 / v_pk_max_u16 advances two window starts.  With q = p (bright) or
-// 255 - p (dark): M1 = (q[2k], q[2k+1]), M2 = min(M1, (q[2k+1], q[2k+2])), M4 = min(M2_k,
-// M2_k+1), M8 = min(M4_k, M4_k+2), and a window of N = 8 + r is min(M8_k, M_r at k + 4).
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-template <int N>
-__device__ __forceinline__ uint32_t score_max_threshold_packed(uint32_t c, const uint32_t (&w)[4],
-                                                               bool dark) {
-    const uint32_t m = dark ? 0xffffffffu : 0u;
-    uint32_t x[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = w[i] ^ m;
-    // q_i is byte i >> 2 of x[i & 3]
-    u16x2 P[8], Q[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int a = 2 * k, b = 2 * k + 1, d = (2 * k + 2) & 15;
-        P[k] = as_u16x2(__builtin_amdgcn_perm(x[b & 3], x[a & 3],
-                                              0x0c000c00u | ((4u + (b >> 2)) << 16) | (a >> 2)));
-        Q[k] = as_u16x2(__builtin_amdgcn_perm(x[d & 3], x[b & 3],
-                                              0x0c000c00u | ((4u + (d >> 2)) << 16) | (b >> 2)));
-    }
-    u16x2 M2[8], M4[8], M8[8], MN[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) M2[k] = __builtin_elementwise_min(P[k], Q[k]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) M4[k] = __builtin_elementwise_min(M2[k], M2[(k + 1) & 7]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) M8[k] = __builtin_elementwise_min(M4[k], M4[(k + 2) & 7]);
-    constexpr int r = N - 8;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int j = (k + 4) & 7;
-        u16x2 t;
-        if constexpr (r == 1) t = P[j];
-        else if constexpr (r == 2) t = M2[j];
-        else if constexpr (r == 3) t = __builtin_elementwise_min(M2[j], P[(k + 5) & 7]);
-        else if constexpr (r == 4) t = M4[j];
-        else if constexpr (r == 5) t = __builtin_elementwise_min(M4[j], P[(k + 6) & 7]);
-        else if constexpr (r == 6) t = __builtin_elementwise_min(M4[j], M2[(k + 6) & 7]);
-        else if constexpr (r == 7)
-            t = __builtin_elementwise_min(__builtin_elementwise_min(M4[j], M2[(k + 6) & 7]), P[(k + 7) & 7]);
-        else t = M8[j];
-        MN[k] = __builtin_elementwise_min(M8[k], t);
-    }
-#pragma unroll
-    for (int s = 4; s >= 1; s >>= 1) {
-#pragma unroll
-        for (int k = 0; k < s; ++k) MN[k] = __builtin_elementwise_max(MN[k], MN[k + s]);
-    }
-    const uint32_t v = as_u32(MN[0]);
-    return max(v & 0xffffu, v >> 16) - (c ^ (m & 0xffu));
 }
 
 // Sum-of-absolute-differences score (src/fast_simd.rs:722-749, scalar :278-299).

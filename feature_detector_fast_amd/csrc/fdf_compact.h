@@ -1,5 +1,5 @@
-// fdf_compact.h -- raster-order compaction of the detector's per-band slots (shared by
-// compact_kernel in fdf_kernels.hip and the fused tail of fast_sweep_kernel in fdf_sweep.hip).
+// fdf_compact.h -- raster-order compaction of the detector's per-band slots (the body of
+// compact_kernel in fdf_kernels.hip).
 //
 // Turns the per-band slots into the reference's output: one list of points per frame, in
 // raster order (src/fast_simd.rs:589-616 pushes keypoints in scan order).  Group g covers

@@ -28,9 +28,15 @@ constexpr uint32_t kFlagNmsPrefixOnly = 32;  // band NMS pass: rank prefixes onl
 constexpr uint32_t kFlagNoEval = 64;       // batches are issued (FIFO, staging, loads), never tested
 #ifdef FDF_DEBUG_BUILD
 __host__ __device__ inline uint32_t ablation_flags(uint32_t f) { return f; }
+constexpr bool kDebugBuild = true;
 #else
 __host__ __device__ inline uint32_t ablation_flags(uint32_t) { return 0u; }
+constexpr bool kDebugBuild = false;
 #endif
+// Debug builds: per-workgroup stamps of the detector (BandParams::stamps, kStampWords words per
+// workgroup): shader clock and 100 MHz real time at the workgroup's start and end, its XCD
+// and hardware id, its band.  Written only to that buffer; no output depends on them.
+constexpr uint32_t kStampWords = 6;
 
 // Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).
@@ -130,10 +136,6 @@ __host__ __device__ inline uint32_t compact_tasks_per_group(uint32_t ntasks) {
     const uint32_t t = ntasks / 1024;
     return t < 1 ? 1u : (t > (uint32_t)kCompactTasks ? (uint32_t)kCompactTasks : t);
 }
-// Grids up to this many bands compact inside the detector launch: the last workgroup to
-// finish (a ticket) orders every band itself, so a single frame costs one launch.
-constexpr uint32_t kFusedCompactTasks = 256;
-
 // Per-group keypoint sums the detector accumulates (one atomic add per band) so that a
 // compaction group finds its output base by summing the groups before it, O(groups) instead
 // of O(tasks).  Two buffers alternate between launches: a launch reads one and its
@@ -170,10 +172,8 @@ struct BandParams {
     uint32_t nstrips, nsub;      // sweep kernel: column strips x sub-bands per band
     uint32_t* group_sums;        // += band count at [task / tasks_per_group] (NULL: none)
     uint32_t tasks_per_group;
-    uint32_t* ticket;            // fused compaction: bands finished (the last one resets it)
-    uint32_t fused;              // 1: the last workgroup runs `compact` (ntasks <= kFusedCompactTasks)
     uint32_t* kp_stats;          // NMS: += each band's keypoints before suppression (NULL: off)
-    CompactParams compact;
+    uint64_t* stamps;            // debug builds: kStampWords per workgroup (NULL: off)
 };
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);

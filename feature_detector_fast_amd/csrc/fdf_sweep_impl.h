@@ -38,7 +38,6 @@
 #include <type_traits>
 
 #include "fdf_common.h"
-#include "fdf_compact.h"
 #include "fdf_kernels.h"
 
 #ifndef FDF_SWEEP_NS
@@ -167,10 +166,6 @@ struct SweepShared {
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
 };
 
-// max-t list entries whose score is computed by the NMS pass: score field kScorePending |
-// polarity (1 = dark); real scores are <= 255
-constexpr uint32_t kScorePending = 0x800u;
-
 struct UnitCtx {
     RowSource src;
     uint32_t t, nw;
@@ -182,11 +177,9 @@ struct UnitCtx {
     int ys;                // first row the unit sweeps (FIFO rows are relative to it)
     int rowbase;           // (ys - 3) * W: frame offset of the window row y - 3 for FIFO row 0
     uint32_t flags;        // BandParams::flags (ablation runs only)
-#ifndef FDF_NO_KP_QUEUE
     // max-t keypoint queue (one entry per lane, kq_n < 64 entries, wave-uniform): the packed
     // ring and pos << 12 | dark << 8 | centre of keypoints whose score is not computed yet
     uint32_t kq_w[4], kq_c, kq_n;
-#endif
 };
 
 // ---------------------------------------------------------------------------------------
@@ -322,35 +315,6 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             const uint32_t excl = inc - k;
             uint32_t m = e & 0xffffu;
             uint32_t scode = 0;
-            (void)scode;
-#if defined(FDF_BALLOT_EXPAND) || defined(FDF_EXPAND_LOOP)
-            uint32_t pos = excl;
-            const uint32_t rl = (e >> 16) << 4;       // (row - ys) << 10 | lane << 4
-#endif
-#ifdef FDF_BALLOT_EXPAND
-            for (;;) {
-                const bool wr = m != 0u && pos < 64u;
-                if (wave_ballot(wr) == 0) break;
-                if (wr) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    sh.stage[pos] = rl | ((bit & 3u) << 2) | (bit >> 2);
-                    ++pos;
-                }
-            }
-#elif defined(FDF_EXPAND_LOOP)
-            // this lane writes min(k, 64 - excl) pixels; a wave-uniform loop over the most
-            // any lane writes (no per-iteration ballot)
-            const uint32_t cnt = excl < 64u ? min(k, 64u - excl) : 0u;
-            const uint32_t iters = __builtin_amdgcn_readfirstlane(wave_max(cnt));
-            for (uint32_t it = 0; it < iters; ++it) {
-                if (it < cnt) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    sh.stage[pos + it] = rl | ((bit & 3u) << 2) | (bit >> 2);
-                }
-            }
-#else
             // no per-pixel loop: entry lane e marks the slot its pixels start at, a wave
             // prefix-max turns the marks into each batch lane's entry, and the lane selects
             // its bit of that entry's mask (binary search over popcounts)
@@ -378,7 +342,6 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             // replaces a second select
             if (has && excl < 64u && inc > 64u)
                 m &= ~0u << (__builtin_amdgcn_readlane(bit, 63) + 1u);
-#endif
             // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
             const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
             if (has && excl < 64u && inc > 64u)
@@ -386,11 +349,7 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
             u.head += nfull;
             b.act = lane < b.n;
             if (b.act) {
-#if defined(FDF_BALLOT_EXPAND) || defined(FDF_EXPAND_LOOP)
-                const uint32_t sc = sh.stage[lane];
-#else
                 const uint32_t sc = scode;
-#endif
                 b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
                 // rows relative to the unit (< 2^10) times W (< 2^16): a 24-bit multiply
                 o = u.rowbase + (int)__umul24(sc >> 10, (uint32_t)W) + u.S - LC + (int)(sc & 1023u);
@@ -437,7 +396,6 @@ __device__ __forceinline__ void append_scores(const SweepShared& sh, const UnitC
     }
 }
 
-#ifndef FDF_NO_KP_QUEUE
 // Scores the first n entries of the max-t keypoint queue (one per lane) and lists them.
 template <int N>
 __device__ __forceinline__ void score_kp_queue(const SweepShared& sh, UnitCtx& u, uint32_t n) {
@@ -453,7 +411,6 @@ __device__ __forceinline__ void score_kp_queue(const SweepShared& sh, UnitCtx& u
     append_scores(sh, u, act, n >= 64 ? ~0ull : (1ull << n) - 1ull,
                   (u.kq_c & 0xfffff000u) | score);
 }
-#endif
 
 template <int NMS, int N, int LC>
 __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u,
@@ -472,7 +429,6 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
     // every queued pixel is a centre of the unit's strip and tested rows (vmask, p0 .. p1)
     const bool is_kp = b.act && (kb || kd);
     if (is_kp) atomicOr(&sh.bitmap[__umul24((uint32_t)(y - u.yb), u.nw) + ((uint32_t)x >> 5)], 1u << (x & 31));
-#ifndef FDF_NO_KP_QUEUE
     if constexpr (NMS == kNmsMaxThreshold) {
         // ~28% of a batch's lanes are keypoints (S1), and the max-t score is ~100 VALU on
         // every lane: keypoints move into the wave's queue (lane q + rank, via the staging
@@ -511,8 +467,7 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
         }
         return;
     }
-#endif
-    if constexpr (NMS != kNmsOff) {
+    if constexpr (NMS == kNmsSumAbsolute) {
         // scores go to the band's LDS list, past its capacity to the band's slot (global),
         // past that they are only counted (the band NMS pass then recomputes all scores)
         const uint64_t bal = wave_ballot(is_kp);
@@ -521,30 +476,7 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
             if (u.lane == 0) base = atomicAdd(sh.slist_n, (uint32_t)__popcll(bal));
             base = __builtin_amdgcn_readfirstlane(base);
             if (is_kp) {
-                uint32_t score;
-                if constexpr (NMS == kNmsMaxThreshold) {
-#ifndef FDF_DEFER_MAXT_SCORE
-#ifdef FDF_MAXT_PACKED
-                    // over u16 pairs (fdf_common.h): 1080p +0.6%, 4K max-t -1.8% (A/B
-                    // profiles/r02/ab_maxt_packed_*), so not the default
-                    score = score_max_threshold_packed<N>(c, w, kd);
-#else
-                    uint32_t p[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
-                    score = score_max_threshold<N>(c, p, kd);
-#endif
-#else
-                    // deferred (FDF_DEFER_MAXT_SCORE): only keypoints with a neighbouring
-                    // keypoint ever need their score (~28% of a batch's lanes are keypoints),
-                    // so the band NMS pass computes it then, one keypoint per lane
-                    // (nms_scatter).  Measured slower: 1080p max-t +0.9%, 4K max-t +6.6%
-                    // (the NMS pass waits on its gathers)
-                    score = kScorePending | (kd ? 1u : 0u);
-#endif
-                } else {
-                    score = score_sum_abs_packed(c, w, u.t);
-                }
+                const uint32_t score = score_sum_abs_packed(c, w, u.t);
                 const uint32_t idx = base + lanes_below(bal);
                 const uint32_t e = ((((uint32_t)(y - u.yb) & 0x3ffu) * (u.src.W & 0xffffffu) + (uint32_t)x) << 12) | score;
                 if (idx < sh.slist_cap) sh.slist[idx] = e;
@@ -560,11 +492,7 @@ struct RowFlags {
     typename LaneRow<LC>::type b, nd;
 };
 
-// Pre-filter comparisons of one lane row (bit 7 of each byte).  FDF_SHARED_LERP: one first
-// lerp for both polarities (fdf_common.h lerp_consts kb0/kd0): `b` flags are a superset of
-// x - c > t and `nd` flags a subset of NOT(x - c < -t), so the cardinal test only gains
-// candidates -- 8 lerps a step fewer, but more candidates on images with exact-threshold
-// steps (measured slower on S1).  Default: the exact comparisons.
+// Pre-filter comparisons of one lane row (bit 7 of each byte), exact (fdf_common.h).
 template <int LC>
 __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>::type& x,
                                                      const typename LaneRow<LC>::type& nc,
@@ -572,14 +500,8 @@ __device__ __forceinline__ RowFlags<LC> compare_rows(const typename LaneRow<LC>:
     RowFlags<LC> f;
 #pragma unroll
     for (int m = 0; m < LC / 4; ++m) {
-#ifdef FDF_SHARED_LERP
-        const uint32_t v = lerp_u8(x[m], nc[m], 0u);
-        f.b[m] = lerp_u8(v, k.kb0, 0);
-        f.nd[m] = lerp_u8(v, k.kd0, 0);
-#else
         f.b[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rb), k.kb, 0);   // x - c > t
         f.nd[m] = lerp_u8(lerp_u8(x[m], nc[m], k.rd), k.kd, 0);  // NOT(x - c < -t)
-#endif
     }
     return f;
 }
@@ -598,13 +520,9 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
         }
     }
     if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;
-#ifndef FDF_PIPELINED_FLUSH_ALL
     // max-t measured 0.6-1.0% slower with the pipelined flush (its keypoint queue and score
     // keep more registers live), NMS off and SAD 0.2-1.5% faster (profiles/r02/ab_flush_rowdiv.txt)
     constexpr bool serial = NMS == kNmsMaxThreshold;
-#else
-    constexpr bool serial = false;
-#endif
     if constexpr (serial) {
         if (inflight[QL]) evaluate_batch<NMS, N, LC>(sh, u, lk, batch[QL]);
         inflight[QL] = false;
@@ -685,11 +603,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
     // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
     // their candidates masked: a branch around it costs the zeroing of `cand` on every step.
-#ifdef FDF_LIVE_BRANCH
-#define FDF_LIVE_TEST(l) (l)
-#else
-#define FDF_LIVE_TEST(l) true
-#endif
 #define FDF_SWEEP_STEP(J)                                                                    \
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
@@ -700,7 +613,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
         const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
-        if (FDF_LIVE_TEST(live)) {                                                           \
+        {                                                                                    \
             RowV e;                                                                          \
             _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
             e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
@@ -783,7 +696,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         }
     }
 #undef FDF_SWEEP_STEP
-#undef FDF_LIVE_TEST
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
@@ -940,36 +852,15 @@ __device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap
     return (e & ~0xfffu) | (suppressed ? 1u : 0u);
 }
 
-// Max-threshold score of the keypoint at (x, y) of known polarity, from the frame (the
-// sweep's windows and packing; deferred scores, see evaluate_batch).
-template <int N>
-__device__ __forceinline__ uint32_t keypoint_score_maxt(const __amdgpu_buffer_rsrc_t& rs, int W,
-                                                        int x, int y, bool dark) {
-    Batch b;
-    load_ring_windows(b, rs, (y - 3) * W + x, W);
-    uint32_t w[4], c;
-    pack_ring(b, w, c);
-    uint32_t p[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = (w[i & 3] >> (8 * (i >> 2))) & 0xffu;
-    return score_max_threshold<N>(c, p, dark);
-}
-
 // Rank-order scatter of list entry e: a keypoint with a neighbouring keypoint puts its score
-// at its raster rank (computing it first when it was deferred); an isolated one is kept
-// without comparison, marked by a zero score.
-template <int NMS, int N, bool RANKED = false>
+// at its raster rank; an isolated one is kept without comparison, marked by a zero score.
+template <bool RANKED = false>
 __device__ __forceinline__ uint32_t nms_scatter(uint32_t e, const uint32_t* bitmap, uint32_t nw,
                                                 uint32_t R2, uint32_t nb_blocks, RowDiv W,
-                                                uint32_t y0, uint16_t* sranked,
-                                                const uint16_t* bprefix, const uint32_t* rprefix,
-                                                const __amdgpu_buffer_rsrc_t& frame) {
+                                                uint16_t* sranked, const uint16_t* bprefix,
+                                                const uint32_t* rprefix) {
     const uint32_t pos = e >> 12, row = udiv(pos, W), x = pos - row * W;
     if (neighbour_bits(bitmap, nw, R2, row, x) == 0) return e & ~0xfffu;
-    if constexpr (NMS == kNmsMaxThreshold) {
-        if (e & kScorePending)
-            e = (e & ~0xfffu) | keypoint_score_maxt<N>(frame, (int)W, (int)x, (int)(y0 - 1 + row), e & 1u);
-    }
     const uint32_t rank = bitmap_rank(bitmap, bprefix, rprefix, nw, nb_blocks, row, x);
     sranked[rank] = (uint16_t)(e & 0xfffu);
     if constexpr (RANKED) return (e & ~0xfffu) | (rank + 1u);
@@ -1001,15 +892,14 @@ __device__ __forceinline__ bool in_band_rows(uint32_t e, RowDiv W, uint32_t R2) 
 template <int NMS, int N>
 __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, RowDiv W,
                              uint32_t H, uint32_t* slist, uint32_t n, uint16_t* sranked,
-                             uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags,
-                             __amdgpu_buffer_rsrc_t frame) {
+                             uint16_t* bprefix, uint32_t* rprefix, uint32_t* total, uint32_t flags) {
     const uint32_t tid = threadIdx.x;
     const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
     band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);
     if (flags & kFlagNmsPrefixOnly) return;
     for (uint32_t i = tid; i < n; i += kThreads)
-        slist[i] = nms_scatter<NMS, N, true>(slist[i], bitmap, nw, R2, nb_blocks, W, y0, sranked,
-                                             bprefix, rprefix, frame);
+        slist[i] = nms_scatter<true>(slist[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix,
+                                     rprefix);
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) {
         const uint32_t e = slist[i];
@@ -1027,7 +917,7 @@ template <int NMS, int N>
 __device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint32_t y0, RowDiv W,
                                uint32_t H, const uint32_t* slist, uint32_t cap, uint32_t* spill,
                                uint32_t n, uint16_t* sranked, uint16_t* bprefix, uint32_t* rprefix,
-                               uint32_t* total, __amdgpu_buffer_rsrc_t frame) {
+                               uint32_t* total) {
     const uint32_t tid = threadIdx.x;
     const uint32_t R2 = rows + 2, nb_blocks = (nw + kRankBlock - 1) / kRankBlock;
     uint32_t ent[kSpillPer];
@@ -1036,11 +926,9 @@ __device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
     band_rank_prefixes(bitmap, R2, nw, bprefix, rprefix, total);   // barriers: list area free
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j)
-        ent[j] = nms_scatter<NMS, N>(ent[j], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
-                                     rprefix, frame);
+        ent[j] = nms_scatter(ent[j], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
     for (uint32_t i = tid; i < n - cap; i += kThreads)
-        spill[i] = nms_scatter<NMS, N>(spill[i], bitmap, nw, R2, nb_blocks, W, y0, sranked, bprefix,
-                                       rprefix, frame);
+        spill[i] = nms_scatter(spill[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix, rprefix);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j)
@@ -1134,7 +1022,6 @@ __device__ __forceinline__ uint32_t band_task(const BandParams& P) {
     const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
     const uint32_t c0 = k8 * q8 + min(k8, r8), j = b >> 3;
     uint32_t task = c0 + j;
-#ifndef FDF_RASTER_DISPATCH
     {
         const uint32_t c1 = c0 + q8 + (k8 < r8 ? 1u : 0u);
         const uint32_t B = P.bands_per_frame;
@@ -1149,7 +1036,6 @@ __device__ __forceinline__ uint32_t band_task(const BandParams& P) {
             }
         }
     }
-#endif
     return task;
 }
 
@@ -1212,9 +1098,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
 
     const uint32_t nunits = P.nstrips * P.nsub;
     const uint32_t sub_rows = (rows + P.nsub - 1) / P.nsub;
-#ifndef FDF_NO_KP_QUEUE
     u.kq_n = 0;
-#endif
     // units are handed out dynamically: a wave that finishes early takes the next one
     // instead of idling at the workgroup barrier
     if (!(ablation_flags(P.flags) & kFlagNoPrefilter)) {
@@ -1245,11 +1129,9 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
                 sweep_unit<NMS, N, false>(sh, u, lk);
             }
         }
-#ifndef FDF_NO_KP_QUEUE
         // the band's last keypoints: a partial queue (once per wave and band)
         if constexpr (NMS == kNmsMaxThreshold)
             if (u.kq_n != 0) score_kp_queue<N>(sh, u, u.kq_n);
-#endif
     }
     __syncthreads();
 
@@ -1264,14 +1146,13 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
                                  reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                                  reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
                                  reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
-                                 ablation_flags(P.flags), rs_exact);
+                                 ablation_flags(P.flags));
         } else if (n - sh.slist_cap <= sh.spill_cap && n <= L.nms_area_entries) {
             // more keypoints than the LDS list holds: the rest were appended to the slot
             band_nms_spill<NMS, N>(bitmap, rows, nw, y0, Wd, H, sh.slist, sh.slist_cap, sh.spill, n,
                                    reinterpret_cast<uint16_t*>(smem_raw + L.pq),
                                    reinterpret_cast<uint16_t*>(smem_raw + L.bprefix),
-                                   reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2,
-                                   rs_exact);
+                                   reinterpret_cast<uint32_t*>(smem_raw + L.rprefix), unit_ctr + 2);
         } else {
             band_nms_dense<NMS, N>(bitmap, rows, nw, y0, W,
                                    reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes),
@@ -1288,46 +1169,6 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     const uint32_t* keep = bitmap + halo * nw;
 
     // ---- count keep-bits and write the band slot
-#ifdef FDF_EMIT_PER_THREAD
-    const uint32_t per = (nwords + kThreads - 1) / kThreads;
-    const uint32_t w_lo = min(tid * per, nwords), w_hi = min(w_lo + per, nwords);
-    uint32_t mine = 0;
-    for (uint32_t w = w_lo; w < w_hi; ++w) mine += __popc(keep[w]);
-    uint32_t incl = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl += o;
-    }
-    if (lane == 63) wave_sum[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        const uint32_t v = wave_sum[w];
-        before += (uint32_t)w < wave ? v : 0u;
-        total += v;
-    }
-    if (ablation_flags(P.flags) & kFlagNoEmit) return total;
-    uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
-    if (total <= P.slot_bytes / 8) {
-        uint2* pts = reinterpret_cast<uint2*>(slot);
-        uint32_t idx = before + incl - mine;
-        for (uint32_t w = w_lo; w < w_hi; ++w) {
-            uint32_t bits = keep[w];
-            const uint32_t r = udiv(w, nwd);
-            const uint32_t xb = (w - r * nw) * 32;
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
-                pts[idx++] = make_uint2(xb + bit, y0 + r);
-            }
-        }
-    } else {
-        uint32_t* words = reinterpret_cast<uint32_t*>(slot);
-        for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
-    }
-#else
     // Each wave owns a contiguous quarter of the bitmap and sweeps it 64 words per round (lane
     // = word): the word reads are independent and conflict-free, and a wave prefix sum of the
     // words' keypoint counts places the round's points consecutively in the slot.
@@ -1369,7 +1210,6 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         uint32_t* words = reinterpret_cast<uint32_t*>(slot);
         for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
     }
-#endif
     return total;
 }
 
@@ -1379,6 +1219,13 @@ __global__ __launch_bounds__(kThreads)
 __attribute__((amdgpu_waves_per_eu(kSweepWavesPerEU, kSweepWavesPerEU)))
 void fast_sweep_kernel(BandParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    uint64_t t0 = 0, r0 = 0;
+    if constexpr (kDebugBuild) {   // workgroup timeline stamps (tools/stamps.py)
+        if (P.stamps) {
+            t0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
     const uint32_t task = band_task(P);
     const uint32_t total = sweep_band<NMS, N>(P, smem_raw, task);
     const uint32_t tid = threadIdx.x;
@@ -1386,28 +1233,24 @@ void fast_sweep_kernel(BandParams P) {
         P.counts[task] = total;
         if (P.group_sums) atomicAdd(&P.group_sums[task / P.tasks_per_group], total);
     }
-#ifdef FDF_FUSED_COMPACT
-    if (P.fused) {
-        // fused compaction (small grids): every band publishes its slot and count, and the
-        // last one to finish (a ticket) orders them all
-        __threadfence();
-        __syncthreads();
-        uint32_t* last = reinterpret_cast<uint32_t*>(smem_raw);
-        if (tid == 0) *last = atomicAdd(P.ticket, 1u) == P.ntasks - 1u ? 1u : 0u;
-        __syncthreads();
-        if (*last) {
-            __threadfence();
+    if constexpr (kDebugBuild) {
+        if (P.stamps) {
             __syncthreads();
-            CompactShared& sm = *reinterpret_cast<CompactShared*>(smem_raw + 16);
-            const uint32_t ngroups = (P.ntasks + P.compact.tasks_per_group - 1) / P.compact.tasks_per_group;
-            for (uint32_t g = 0; g < ngroups; ++g) {
-                compact_group(P.compact, g, sm);
-                __syncthreads();
+            if (tid == 0) {
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+                uint64_t* s = P.stamps + (uint64_t)blockIdx.x * kStampWords;
+                s[0] = t0;
+                s[1] = t1;
+                s[2] = r0;
+                s[3] = r1;
+                // HW_REG_XCC_ID (20) and HW_REG_HW_ID (4), whole registers
+                s[4] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) |
+                       (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
+                s[5] = task;
             }
-            if (tid == 0) *P.ticket = 0u;           // for the next launch
         }
     }
-#endif
 }
 
 typedef void (*SweepKernelFn)(BandParams);

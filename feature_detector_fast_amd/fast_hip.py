@@ -212,7 +212,10 @@ def detector_batch(frames, config, device=0, devices=None):
     cap = capacity_guess(f * h * w)
     out = np.empty((cap, 2), dtype=np.uint32)
     n = ctypes.c_size_t(0)
-    for c in ctxs:
+    # one global lock order (by handle), whatever order the caller lists the devices in:
+    # detector_batch(devices=[0, 1]) and devices=[1, 0] from two threads cannot deadlock
+    locked = sorted(ctxs, key=lambda c: c.handle.value)
+    for c in locked:
         c.lock.acquire()
     try:
         rc = lib.fdf_detect_batch_multi(handles, len(ctxs), ptr, f, w, h, h * w,
@@ -225,7 +228,7 @@ def detector_batch(frames, config, device=0, devices=None):
                                           ctypes.byref(n))
             where = "fdf_fetch_last_multi"
     finally:
-        for c in ctxs:
+        for c in reversed(locked):
             c.lock.release()
     check(rc, where)
     return out[: n.value], offsets
@@ -296,9 +299,13 @@ def keypoint_scores(img, points, config, device=0):
     cfg = _to_c_config(config)
     h, w = arr.shape
     scores = np.zeros(pts.shape[0], dtype=np.uint16)
-    rc = _native.load().fdf_score_points(
-        context(device).handle, arr.ctypes.data, w, h, arr.strides[0], ctypes.byref(cfg),
-        pts.ctypes.data, pts.shape[0], scores.ctypes.data)
+    ctx = context(device)
+    # fdf_score_points reuses the context's retained result buffers: hold the lock that keeps
+    # a two-call pattern (detect, then fdf_fetch_last) of another thread together
+    with ctx.lock:
+        rc = _native.load().fdf_score_points(
+            ctx.handle, arr.ctypes.data, w, h, arr.strides[0], ctypes.byref(cfg),
+            pts.ctypes.data, pts.shape[0], scores.ctypes.data)
     check(rc, "fdf_score_points")
     return scores
 
@@ -320,8 +327,10 @@ def score_rings(centers, rings, score, threshold=0, consecutive=9, device=0):
         raise ValueError("threshold must fit u8")
     cfg = _ring_config(score, threshold, consecutive)
     out = np.zeros(c.shape[0], dtype=np.uint16)
-    rc = _native.load().fdf_score_rings(context(device).handle, c.ctypes.data, r.ctypes.data,
-                                        c.shape[0], ctypes.byref(cfg), out.ctypes.data)
+    ctx = context(device)
+    with ctx.lock:   # reuses the retained result buffers, see keypoint_scores
+        rc = _native.load().fdf_score_rings(ctx.handle, c.ctypes.data, r.ctypes.data,
+                                            c.shape[0], ctypes.byref(cfg), out.ctypes.data)
     check(rc, "fdf_score_rings")
     return out
 
@@ -347,10 +356,18 @@ def score_rings_device(centers, rings, scores, score, threshold=0, consecutive=9
     if rings.dim() != 2 or rings.shape[1] != 16 or centers.numel() != rings.shape[0] \
             or scores.numel() < rings.shape[0]:
         raise ValueError("rings must be (K, 16) with K centres and K scores")
+    if centers.dtype != torch.uint8 or rings.dtype != torch.uint8:
+        raise ValueError("centers and rings must be uint8 tensors")
+    if not (centers.is_cuda and rings.is_cuda and scores.is_cuda):
+        raise ValueError("score_rings_device needs CUDA (HIP) tensors")
+    if not (centers.device == rings.device == scores.device):
+        raise ValueError("centers, rings and scores must be on the same device")
     if not (centers.is_contiguous() and rings.is_contiguous() and scores.is_contiguous()):
         raise ValueError("tensors must be contiguous")
     if scores.element_size() != 2:
         raise ValueError("scores must be a 16-bit tensor")
+    if rings.numel() and rings.data_ptr() % 16 != 0:
+        raise ValueError("rings must start on a 16-byte boundary (one 16-byte load per ring)")
     dev = rings.device.index if device is None else device
     cfg = _ring_config(score, threshold, consecutive)
     if stream is None:

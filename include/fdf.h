@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FDF_ABI_VERSION 3
+#define FDF_ABI_VERSION 4
 
 /* Status codes.  Shapes the reference maps to an empty Vec return FDF_OK with 0 points. */
 enum fdf_status {
@@ -104,6 +104,13 @@ int fdf_ctx_timing_samples(fdf_ctx* ctx, float* detect_ms, float* compact_ms, ui
  * large batches -- the parity tests reach those code paths with small inputs this way. */
 int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
 
+/* Band height override: every later detection on the context sweeps bands of `rows` centre
+ * rows (rounded up to the geometry's sub-band multiple, capped by what the workgroup's LDS
+ * holds, 160 KB); 0 restores the automatic choice (LDS budget, grid size, and for NMS the
+ * keypoint density of the previous launch).  The keypoints are the same at every height;
+ * tests use it to cross the band NMS pass's LDS / spill / dense tiers. */
+int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows);
+
 /* Device bytes the context's workspace holds now (host-API staging and output, per-band
  * slots and counts, compaction sums).  Slots take 1/8 byte per pixel of the largest batch
  * seen; nothing in the workspace scales with more than that. */
@@ -169,13 +176,17 @@ int fdf_detect_batch(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint3
  * detected on ctxs[k] by its own host thread (contexts may be on different devices, or
  * several on one), and the lists are concatenated in frame order -- the same result as
  * fdf_detect_batch on one context.  The contexts must be distinct.  Capacity semantics as
- * fdf_detect_batch; each context keeps its shard for fdf_fetch_last_multi.
+ * fdf_detect_batch; each context keeps its shard for fdf_fetch_last_multi.  The contexts are
+ * locked in one global order, so concurrent calls over the same contexts listed in different
+ * orders do not deadlock.
  */
 int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* data,
                            uint32_t n_frames, uint32_t width, uint32_t height,
                            size_t frame_stride_bytes, const fdf_config* cfg, fdf_point* out,
                            size_t cap, uint64_t* frame_offsets, size_t* n_out);
-/* fdf_fetch_last over the contexts of the last fdf_detect_batch_multi, concatenated. */
+/* fdf_fetch_last over the contexts of the last fdf_detect_batch_multi, concatenated.  The
+ * contexts must hold the shards of ONE such call, passed in that call's order; otherwise (a
+ * host call on one of them since, another multi call, a reordered array) FDF_ERR_ARG. */
 int fdf_fetch_last_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, fdf_point* out, size_t cap,
                          size_t* n_out);
 

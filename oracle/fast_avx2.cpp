@@ -15,6 +15,9 @@
 #include <cstdint>
 #include <cstring>
 #include <thread>
+
+#include <pthread.h>
+#include <sched.h>
 #include <vector>
 
 namespace {
@@ -262,12 +265,19 @@ int64_t fdf_avx2_detect(const uint8_t* data, uint32_t w, uint32_t h, uint8_t t, 
 // Times `reps` passes over `n_frames` frames (frame f at frames + f * frame_stride, each
 // padded as above), spreading frames over `threads` std::threads.  Returns wall seconds
 // and the keypoint total of one pass in *total.
-double fdf_avx2_time(const uint8_t* frames, uint32_t n_frames, size_t frame_stride,
-                     uint32_t w, uint32_t h, uint8_t t, uint8_t n, uint8_t nms, int threads,
-                     int reps, uint64_t* total) {
+// With `cpus` (threads entries), worker i pins itself to CPU cpus[i] before it starts.
+double fdf_avx2_time_pinned(const uint8_t* frames, uint32_t n_frames, size_t frame_stride,
+                            uint32_t w, uint32_t h, uint8_t t, uint8_t n, uint8_t nms,
+                            int threads, int reps, const int* cpus, uint64_t* total) {
     if (threads < 1) threads = 1;
     std::vector<uint64_t> counts(threads, 0);
     auto worker = [&](int tid) {
+        if (cpus) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            CPU_SET(cpus[tid], &set);
+            (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+        }
         uint64_t c = 0;
         for (int rep = 0; rep < reps; ++rep) {
             for (uint32_t f = tid; f < n_frames; f += threads) {
@@ -291,6 +301,13 @@ double fdf_avx2_time(const uint8_t* frames, uint32_t n_frames, size_t frame_stri
     for (uint64_t c : counts) sum += c;
     if (total) *total = sum;
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+double fdf_avx2_time(const uint8_t* frames, uint32_t n_frames, size_t frame_stride,
+                     uint32_t w, uint32_t h, uint8_t t, uint8_t n, uint8_t nms, int threads,
+                     int reps, uint64_t* total) {
+    return fdf_avx2_time_pinned(frames, n_frames, frame_stride, w, h, t, n, nms, threads, reps,
+                                nullptr, total);
 }
 
 // Criterion-like single-frame protocol (benches/benchmark.rs:18-50): `warmup` untimed

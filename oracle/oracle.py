@@ -74,6 +74,10 @@ def _load_avx2():
         lib.fdf_avx2_time.argtypes = [ctypes.c_void_p, u32, ctypes.c_size_t, u32, u32, u8, u8,
                                       u8, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_uint64)]
+        lib.fdf_avx2_time_pinned.restype = ctypes.c_double
+        lib.fdf_avx2_time_pinned.argtypes = [ctypes.c_void_p, u32, ctypes.c_size_t, u32, u32, u8,
+                                             u8, u8, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_uint64)]
         lib.fdf_avx2_samples.restype = ctypes.c_int64
         lib.fdf_avx2_samples.argtypes = [ctypes.c_void_p, u32, u32, u8, u8, u8, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_void_p]
@@ -183,16 +187,24 @@ def avx2_detect(img, t, n, nms):
     return out
 
 
-def avx2_time(frames, t, n, nms, threads=1, reps=1):
-    """Wall seconds for `reps` passes over a (F, H, W) stack with `threads` workers, and the
+def avx2_time(frames, t, n, nms, threads=1, reps=1, cpus=None):
+    """Wall seconds for `reps` passes over a (F, H, W) stack with `threads` workers (frame f
+    on worker f % threads; worker i pinned to CPU cpus[i] when `cpus` is given), and the
     keypoint total of one pass."""
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
     f, h, w = frames.shape
     buf = np.zeros(frames.size + 16, dtype=np.uint8)
     buf[: frames.size] = frames.reshape(-1)
     total = ctypes.c_uint64(0)
-    secs = _load_avx2().fdf_avx2_time(buf.ctypes.data, f, h * w, w, h, t, n, int(nms), threads,
-                                      reps, ctypes.byref(total))
+    lib = _load_avx2()
+    if cpus is None:
+        secs = lib.fdf_avx2_time(buf.ctypes.data, f, h * w, w, h, t, n, int(nms), threads,
+                                 reps, ctypes.byref(total))
+    else:
+        cpu_arr = np.ascontiguousarray(np.asarray(cpus, dtype=np.int32)[:threads])
+        assert cpu_arr.size == threads
+        secs = lib.fdf_avx2_time_pinned(buf.ctypes.data, f, h * w, w, h, t, n, int(nms), threads,
+                                        reps, cpu_arr.ctypes.data, ctypes.byref(total))
     return secs, int(total.value)
 
 

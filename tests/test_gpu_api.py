@@ -175,3 +175,121 @@ def test_multi_device_rejects_repeated_context():
     rc = lib.fdf_detect_batch_multi(handles, 2, frames.ctypes.data, 2, 20, 20, 400,
                                     ctypes.byref(cfg), None, 0, None, ctypes.byref(n))
     assert rc == _native.FDF_ERR_ARG
+
+
+def _multi(lib, handles, frames, cfg, out, offs, n):
+    f, h, w = frames.shape
+    return lib.fdf_detect_batch_multi(handles, len(handles), frames.ctypes.data, f, w, h, h * w,
+                                      ctypes.byref(cfg), out.ctypes.data if out is not None else None,
+                                      0 if out is None else out.shape[0],
+                                      offs.ctypes.data, ctypes.byref(n))
+
+
+def test_multi_device_reversed_orders_do_not_deadlock():
+    """Two threads run fdf_detect_batch_multi over the same two contexts listed in opposite
+    orders: the contexts are locked in one global order, so both finish, and
+    each result equals the oracle in its own shard order."""
+    import threading
+
+    lib = _native.load()
+    a, b = _native.Context(0), _native.Context(0)
+    frames = np.stack([workloads.s1_frame(i, 320, 240) for i in range(4)])
+    want = [oracle.detect(frames[f], 16, 9, 1) for f in range(4)]
+    cfg = _native.FdfConfig(16, 9, 1)
+    errors = []
+
+    def run(order):
+        handles = (ctypes.c_void_p * 2)(*[c.handle.value for c in order])
+        for _ in range(20):
+            out = np.zeros((4 * 320 * 240 // 8, 2), dtype=np.uint32)
+            offs = np.zeros(5, dtype=np.uint64)
+            n = ctypes.c_size_t(0)
+            rc = _multi(lib, handles, frames, cfg, out, offs, n)
+            if rc != _native.FDF_OK:
+                errors.append(rc)
+                return
+            for f in range(4):
+                if not np.array_equal(out[offs[f]:offs[f + 1]], want[f]):
+                    errors.append(("frame", f))
+                    return
+
+    ts = [threading.Thread(target=run, args=(o,)) for o in ((a, b), (b, a))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=90)
+    alive = any(t.is_alive() for t in ts)
+    assert not alive, "fdf_detect_batch_multi deadlocked"
+    a.close()
+    b.close()
+    assert not errors, errors
+
+
+def test_fetch_last_multi_checks_the_call():
+    """fdf_fetch_last_multi joins only the shards of one fdf_detect_batch_multi call in its
+    order: a reordered array, or a host call on one context in between, is FDF_ERR_ARG
+    (ADVICE r02); the matching array gets the oracle's lists."""
+    lib = _native.load()
+    a, b = _native.Context(0), _native.Context(0)
+    frames = np.stack([workloads.s1_frame(i, 320, 240) for i in range(3)])
+    cfg = _native.FdfConfig(16, 9, 0)
+    ab = (ctypes.c_void_p * 2)(a.handle.value, b.handle.value)
+    ba = (ctypes.c_void_p * 2)(b.handle.value, a.handle.value)
+    offs = np.zeros(4, dtype=np.uint64)
+    n = ctypes.c_size_t(0)
+    assert _multi(lib, ab, frames, cfg, None, offs, n) == _native.FDF_ERR_CAPACITY
+    total = n.value
+    out = np.zeros((total, 2), dtype=np.uint32)
+    assert lib.fdf_fetch_last_multi(ba, 2, out.ctypes.data, total, ctypes.byref(n)) == _native.FDF_ERR_ARG
+    assert lib.fdf_fetch_last_multi(ab, 2, out.ctypes.data, total, ctypes.byref(n)) == _native.FDF_OK
+    want = np.concatenate([oracle.detect(frames[f], 16, 9, 0) for f in range(3)])
+    assert n.value == total and np.array_equal(out, want)
+    img = frames[0].copy()
+    one = np.zeros((10000, 2), dtype=np.uint32)
+    assert lib.fdf_detect(a.handle, img.ctypes.data, 320, 240, 320, ctypes.byref(cfg),
+                          one.ctypes.data, 10000, ctypes.byref(n)) == _native.FDF_OK
+    assert lib.fdf_fetch_last_multi(ab, 2, out.ctypes.data, total, ctypes.byref(n)) == _native.FDF_ERR_ARG
+    a.close()
+    b.close()
+
+
+def test_scores_do_not_break_a_concurrent_two_call():
+    """keypoint_scores / score_rings take the context lock that holds detect_array's two-call
+    pattern together: dense detections (fetched with fdf_fetch_last) running
+    beside score calls on the same context stay exact."""
+    import threading
+
+    img = workloads.s3_frame(5)[:300, :400].copy()
+    cfg = Config(16, 9, NonMaximalSuppression.Off)
+    want = oracle.detect(img, 16, 9, 0)
+    assert len(want) > fast_hip.capacity_guess(img.size)
+    pts = want[:500]
+    scfg = Config(16, 9, NonMaximalSuppression.MaxThreshold)
+    want_sc = fast_hip.keypoint_scores(img, pts, scfg)
+    errors = []
+
+    def detect():
+        try:
+            for _ in range(15):
+                if not np.array_equal(fast_hip.detect_array(img, cfg), want):
+                    errors.append("detect")
+        except Exception as e:          # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    def score():
+        try:
+            for _ in range(15):
+                if not np.array_equal(fast_hip.keypoint_scores(img, pts, scfg), want_sc):
+                    errors.append("scores")
+                fast_hip.score_rings(np.zeros(64, np.uint8), np.zeros((64, 16), np.uint8),
+                                     NonMaximalSuppression.SumAbsolute, threshold=3)
+        except Exception as e:          # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=detect), threading.Thread(target=score)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:3]

@@ -148,24 +148,6 @@ def test_lerp_byte_comparisons_exact():
         assert np.array_equal(~not_dark, x < c - t), t
 
 
-def test_lerp_prefilter_comparisons_relaxed():
-    """The sweep's pre-filter shares one lerp between both polarities (compare_rows with
-    lerp_consts().kb0/kd0): its bright flags contain X - c > t and its dark flags contain
-    X - c < -t, widened by at most one grey level, so the cardinal test can only gain
-    candidates."""
-    c = np.arange(256)[:, None]
-    x = np.arange(256)[None, :]
-    for t in range(255):
-        kb0 = 256 - ((t + 256) >> 1)
-        kd0 = 256 - ((256 - t) >> 1)
-        v = _lerp(x, 255 - c, 0)
-        bright = _lerp(v, np.full((256, 256), kb0), 0) >= 128
-        dark = ~(_lerp(v, np.full((256, 256), kd0), 0) >= 128)
-        assert np.all(bright[x > c + t]) and np.all(dark[x < c - t]), t
-        assert np.array_equal(bright, x >= c + t + (t + 1) % 2), t
-        assert np.array_equal(dark, x <= c - t - t % 2), t
-
-
 def _prefilter(ring, c, t, n):
     card = [ring[0], ring[4], ring[8], ring[12]]
     b = [p > c + t for p in card]
@@ -397,43 +379,6 @@ def test_sad_score_packed_identity():
     assert np.array_equal(got, np.maximum(sb, sd))
     for k in range(0, m, 20000):                        # and the literal oracle, sampled
         assert got[k] == oracle.score_sum_abs(int(c[k]), ring[k].tolist(), int(t[k]))
-
-
-def test_max_threshold_packed_pairs():
-    """fdf_common.h score_max_threshold_packed: windows over u16 pairs (register k = window
-    starts 2k, 2k+1; M2, M4, M8 and M_N = min(M8_k, M_r at k+4)) give the reference's max-t
-    score for keypoints, every n = 9..16 (numpy restatement of the same index arithmetic)."""
-    rng = np.random.default_rng(9)
-    m = 20000
-    ring = rng.integers(0, 256, (m, 16)).astype(np.int64)
-    c = rng.integers(0, 256, m).astype(np.int64)
-    near = rng.integers(0, 2, m).astype(bool)
-    ring[near] = np.clip(c[near, None] + rng.integers(-60, 61, (near.sum(), 16)), 0, 255)
-    for n in range(9, 17):
-        t = 10
-        kps = [i for i in range(0, m, 7) if oracle.is_corner(int(c[i]), ring[i].tolist(), t, n)]
-        for i in kps[:300]:
-            p = ring[i]
-            bright = oracle.is_corner(int(c[i]), p.tolist(), t, n) and any(
-                all(p[(s + k) % 16] > c[i] + t for k in range(n)) for s in range(16))
-            q = p if bright else 255 - p
-            P = [(q[2 * k], q[2 * k + 1]) for k in range(8)]
-            Q = [(q[2 * k + 1], q[(2 * k + 2) % 16]) for k in range(8)]
-            pmin = lambda a, b: (min(a[0], b[0]), min(a[1], b[1]))
-            M2 = [pmin(P[k], Q[k]) for k in range(8)]
-            M4 = [pmin(M2[k], M2[(k + 1) % 8]) for k in range(8)]
-            M8 = [pmin(M4[k], M4[(k + 2) % 8]) for k in range(8)]
-            r = n - 8
-            MN = []
-            for k in range(8):
-                j = (k + 4) % 8
-                tt = {1: P[j], 2: M2[j], 3: pmin(M2[j], P[(k + 5) % 8]), 4: M4[j],
-                      5: pmin(M4[j], P[(k + 6) % 8]), 6: pmin(M4[j], M2[(k + 6) % 8]),
-                      7: pmin(pmin(M4[j], M2[(k + 6) % 8]), P[(k + 7) % 8]), 8: M8[j]}[r]
-                MN.append(pmin(M8[k], tt))
-            best = max(max(a, b) for a, b in MN)
-            got = best - (c[i] if bright else 255 - c[i])
-            assert got == oracle.score_max_threshold(int(c[i]), p.tolist(), n), (n, i)
 
 
 def test_rowdiv_multiply_high_division():

@@ -145,3 +145,18 @@ def test_score_rings_device():
     flat = torch.zeros(16 * 4 + 1, dtype=torch.uint8, device="cuda")
     assert lib.fdf_score_rings_device(ctx.handle, dc.data_ptr(), flat.data_ptr() + 1, 4,
                                       ctypes.byref(cfg), out.data_ptr(), None) != 0   # unaligned
+
+
+def test_score_rings_device_argument_checks():
+    """score_rings_device names the failed check before any device call:
+    non-uint8 centres or rings, and tensors that are not CUDA tensors, raise ValueError."""
+    import torch
+    c = torch.zeros(4, dtype=torch.uint8)
+    r = torch.zeros((4, 16), dtype=torch.uint8)
+    s = torch.zeros(4, dtype=torch.int16)
+    with pytest.raises(ValueError, match="uint8"):
+        fast_hip.score_rings_device(c.to(torch.int32), r, s, SAD)
+    with pytest.raises(ValueError, match="uint8"):
+        fast_hip.score_rings_device(c, r.to(torch.int16), s, SAD)
+    with pytest.raises(ValueError, match="CUDA"):
+        fast_hip.score_rings_device(c, r, s, SAD)

@@ -1,0 +1,130 @@
+"""Workgroup timeline of the detector kernel from the debug build's stamps (s_memtime /
+s_memrealtime at each workgroup's start and end, its XCD and CU; fdf_kernels.h kStampWords).
+
+    FDF_LIB_PATH=build/libfdf_debug.so python tools/stamps.py --frames 64 512 --nms maxt
+
+For each batch size: the launch's span (first start to last end, real time), the ramp (time
+until every CU has started a workgroup), the tail (time from the 90th-percentile end to the
+last), workgroup durations, per-XCD spans, the in-kernel shader clock (Δmemtime / Δrealtime x
+100 MHz) and the HIP-event duration of the same launches.  Stamps go to their own buffer; this
+build's times are for shares, not for quoting.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("FDF_LIB_PATH", os.path.join(ROOT, "build", "libfdf_debug.so"))
+os.environ["FDF_STAMPS"] = "1"
+WORDS = 6
+
+
+def summarize(st, ntasks_expected):
+    t0, t1, r0, r1, ids, task = (st[:, k] for k in range(WORDS))
+    xcc = (ids >> 32) & 0xF
+    hw = ids & 0xFFFFFFFF
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 0x1
+    se = (hw >> 13) & 0x7
+    cu_key = xcc * 1000 + se * 100 + sh * 16 + cu
+    base = r0.min()
+    s_us = (r0 - base) / 100.0          # s_memrealtime ticks at 100 MHz
+    e_us = (r1 - base) / 100.0
+    span = float(e_us.max())
+    clocks = (t1 - t0) / np.maximum(r1 - r0, 1) * 100.0   # MHz
+    dur = e_us - s_us
+    first_per_cu = {}
+    for k, s in zip(cu_key, s_us):
+        first_per_cu[k] = min(first_per_cu.get(k, 1e18), s)
+    xcds = {}
+    for x in sorted(set(xcc.tolist())):
+        m = xcc == x
+        xcds[int(x)] = {"wg": int(m.sum()), "start_us": round(float(s_us[m].min()), 2),
+                        "end_us": round(float(e_us[m].max()), 2),
+                        "wg_us_mean": round(float(dur[m].mean()), 2)}
+    order = np.sort(e_us)
+    return {
+        "workgroups": int(len(st)), "ntasks": int(ntasks_expected),
+        "span_us": round(span, 2),
+        "cus_seen": len(first_per_cu),
+        "ramp_us": round(float(max(first_per_cu.values())), 2),
+        "start_us_p50_p90_max": [round(float(np.percentile(s_us, q)), 2) for q in (50, 90, 100)],
+        "end_us_p10_p50_p90": [round(float(np.percentile(e_us, q)), 2) for q in (10, 50, 90)],
+        "tail_us_p90_to_last": round(float(order[-1] - np.percentile(e_us, 90)), 2),
+        "wg_us_p5_p50_p95": [round(float(np.percentile(dur, q)), 2) for q in (5, 50, 95)],
+        "busy_fraction": round(float(dur.sum() / (span * len(first_per_cu) * 4)), 3),
+        "clock_mhz_p50": round(float(np.median(clocks)), 1),
+        "xcd": xcds,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, nargs="+", default=[64, 512])
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--threshold", type=int, default=16)
+    ap.add_argument("--count", type=int, default=9)
+    ap.add_argument("--nms", default="maxt")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--raw", default="", help="write the raw stamps of each batch size here (.npz)")
+    args = ap.parse_args()
+    import torch
+
+    import workloads
+    from feature_detector_fast_amd import Config, NonMaximalSuppression, _native, fast_hip
+
+    lib = _native.load()
+    if not hasattr(lib, "fdf_debug_stamps"):
+        sys.exit("fdf_debug_stamps missing: use the debug build (make debug)")
+    lib.fdf_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    lib.fdf_debug_stamps.restype = ctypes.c_int
+    nms = {"off": 0, "maxt": 1, "sad": 2}[args.nms]
+    cfg = Config(args.threshold, args.count, NonMaximalSuppression(nms))
+    stream = torch.cuda.current_stream()
+    ctx = fast_hip.context(0)
+    res = {}
+    raw = {}
+    for F in args.frames:
+        frames = workloads.s1_frames_torch(0, F, args.width, args.height)
+        # copies so that the batch comes from HBM, not the Infinity Cache (as bench.py)
+        copies = [frames] + [frames.clone() for _ in range(max(0, (1 << 29) // frames.numel()))]
+        out = torch.empty((F * 50_000, 2), dtype=torch.int32, device="cuda")
+        offs = torch.zeros(F + 1, dtype=torch.int64, device="cuda")
+        for k in range(5):
+            fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        per = []
+        for k in range(args.iters):
+            fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+            torch.cuda.synchronize()
+            n = ctypes.c_uint64(0)
+            _native.check(lib.fdf_debug_stamps(ctx.handle, None, 0, ctypes.byref(n)), "stamps")
+            buf = np.zeros(n.value, dtype=np.uint64)
+            _native.check(lib.fdf_debug_stamps(ctx.handle, buf.ctypes.data, n.value,
+                                               ctypes.byref(n)), "stamps")
+            st = buf.reshape(-1, WORDS).astype(np.int64)
+            per.append(summarize(st, st.shape[0]))
+            if k == args.iters - 1:
+                raw[f"f{F}"] = st
+        det, _ = ctx.timing_samples()
+        ctx.set_timing(False)
+        med = sorted(per, key=lambda d: d["span_us"])[len(per) // 2]
+        med["event_ms_p50"] = round(float(np.median(det)), 4)
+        med["span_us_all"] = [p["span_us"] for p in per]
+        res[F] = med
+        del copies, frames, out
+    if args.raw:
+        np.savez_compressed(args.raw, **raw)
+    print(json.dumps({"config": vars(args), "by_frames": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

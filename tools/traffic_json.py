@@ -7,13 +7,18 @@ one) are averaged over the kernel's dispatches.  gfx950 tallies a wide coalesced
 half its bytes (MI355X_MICROARCH.md, HBM/rocprofv3 section), so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 The result is merged into OUT.json under CFG_KEY (bench.py reads it as roofline.traffic).
+Each entry is stamped with the kernel sources it was profiled from (workloads.
+kernel_source_sha16) and the git revision ($FDF_REV, when the caller passes it: the GPU box
+has no .git); bench.py reports an entry of other sources as stale, not as traffic.
 """
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pmc_summary import load  # noqa: E402
+import workloads  # noqa: E402
 
 
 def mean_counter(d, name, kernel):
@@ -35,7 +40,8 @@ def main():
         sys.exit("counters missing")
     entry = {"kernel": kernel, "dispatches": [nf, nw], "FETCH_SIZE_KiB": fetch,
              "WRITE_SIZE_KiB": write, "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
-             "correction": "gfx950: FETCH_SIZE x2 (half-tallied wide reads)"}
+             "correction": "gfx950: FETCH_SIZE x2 (half-tallied wide reads)",
+             "src_sha16": workloads.kernel_source_sha16(), "rev": os.environ.get("FDF_REV")}
     data = {}
     if os.path.exists(out):
         with open(out) as f:
