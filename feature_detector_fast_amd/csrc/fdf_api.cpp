@@ -73,6 +73,10 @@ struct fdf_ctx {
     bool timing = false;
     size_t timed = 0;                     // calls recorded since timing was enabled
     std::vector<hipEvent_t> ev;           // 3 per recorded call, kMaxTimedCalls at most
+    // direct output of small grids (BandParams::direct): look-back descriptors, launch tag
+    uint64_t* d_lookback = nullptr;       size_t lookback_n = 0;
+    uint32_t epoch = 0;
+    uint32_t cus = 0;                     // compute units of the device
     // debug builds (FDF_STAMPS set): the last detector launch's workgroup stamps
     uint64_t* d_stamps = nullptr;         size_t stamps_n = 0;
     uint64_t stamps_used = 0;             // words written by the last launch
@@ -287,8 +291,16 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     // detection and compaction are two launches: a compaction fused into the detector's last
     // workgroup measured 87 us for one frame against 13 + 12 us (every workgroup's device-scope
     // release is an L2 writeback on gfx950)
+    // Small grids write their points directly (look-back, no compaction launch) when every
+    // workgroup is resident at once: 4 per CU (4 waves per SIMD), fewer if LDS-bound
+    const fdfk::SweepLayout lay = fdfk::make_sweep_layout(R, nw, cfg->nms);
+    const uint32_t wg_per_cu = std::min<uint32_t>(4u, fdfk::kSweepMaxLds / std::max(lay.total, 1u));
+    bool direct = ntasks <= std::min<uint64_t>(fdfk::kDirectMaxTasks, (uint64_t)ctx->cus * wg_per_cu);
+#ifdef FDF_DEBUG_BUILD
+    if (const char* e = std::getenv("FDF_DIRECT")) direct = direct && std::strtoul(e, nullptr, 0) != 0;
+#endif
     const uint64_t ngroups = (ntasks + tpg - 1) / tpg;
-    const bool grouped = ngroups <= fdfk::kMaxGroupSums;
+    const bool grouped = !direct && ngroups <= fdfk::kMaxGroupSums;
     uint32_t* sums_now = ctx->d_sums + (size_t)ctx->sums_parity * fdfk::kMaxGroupSums;
     uint32_t* sums_next = ctx->d_sums + (size_t)(1 - ctx->sums_parity) * fdfk::kMaxGroupSums;
     fdfk::BandParams p;
@@ -327,6 +339,21 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.tasks_per_group = tpg;
     p.kp_stats = nullptr;
     p.stamps = nullptr;
+    p.direct = direct ? 1u : 0u;
+    p.epoch = 0;
+    p.lookback = nullptr;
+    p.out = d_out;
+    p.cap = cap;
+    p.frame_offsets = d_offsets;
+    if (direct) {
+        uint64_t* prev = ctx->d_lookback;
+        if ((rc = ensure(ctx, &ctx->d_lookback, &ctx->lookback_n, (size_t)ntasks, stream))) return rc;
+        if (ctx->d_lookback != prev &&   // a new buffer: no stale launch tags
+            hipMemsetAsync(ctx->d_lookback, 0, ctx->lookback_n * sizeof(uint64_t), stream) != hipSuccess)
+            return FDF_ERR_DEVICE;
+        p.lookback = ctx->d_lookback;
+        p.epoch = ++ctx->epoch == 0 ? ++ctx->epoch : ctx->epoch;   // fresh buffers read as 0
+    }
 #ifdef FDF_DEBUG_BUILD
     if (std::getenv("FDF_STAMPS")) {
         const size_t words = (size_t)ntasks * fdfk::kStampWords;
@@ -338,7 +365,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.kp_stats = nullptr;
     c.stats_out = nullptr;
     c.stats_seq = 0;
-    if (cfg->nms && ctx->h_stats) {
+    if (cfg->nms && ctx->h_stats && !direct) {
         const uint32_t seq = ++ctx->stats_seq == 0 ? ++ctx->stats_seq : ctx->stats_seq;
         fdf_ctx::LaunchInfo& li = ctx->hist[seq % 8];
         li.seq = seq;
@@ -368,7 +395,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         return FDF_ERR_DEVICE;
     }
     if (ev && hipEventRecord(ev[1], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    if (fdfk::launch_compact(c, stream) != hipSuccess) {
+    if (!direct && fdfk::launch_compact(c, stream) != hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
@@ -417,7 +444,7 @@ int check_host_args(const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t
 int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
              size_t row_stride, size_t frame_stride, const fdf_config* cfg, bool rgb,
              uint64_t* offs) {
-    ctx->last.valid = false;
+    ctx->last = LastResult{};          // invalid, and not a shard of a multi-context call
     const size_t frame_bytes = (size_t)w * h;
     const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
     // first guess: 1 keypoint per 64 pixels (real images: 0.5-1.5 per 100)
@@ -617,6 +644,8 @@ int fdf_ctx_create(int device, fdf_ctx** out_ctx) {
     if (!ctx) return FDF_ERR_ALLOC;
     ctx->device = device;
     DeviceGuard guard(device);
+    hipDeviceProp_t prop;
+    ctx->cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? (uint32_t)prop.multiProcessorCount : 0u;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FDF_ERR_DEVICE;
@@ -640,6 +669,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_counts);
         (void)hipFree(ctx->d_sums);
         (void)hipFree(ctx->d_stamps);
+        (void)hipFree(ctx->d_lookback);
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         if (ctx->done) (void)hipEventDestroy(ctx->done);
         if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);

@@ -67,6 +67,14 @@ constexpr int kSweepRing = FDF_RING;
 #define FDF_WAVES_PER_EU 4
 #endif
 constexpr int kSweepWavesPerEU = FDF_WAVES_PER_EU;
+// A/B variant (built by tools/build_variant.sh with -DFDF_DIAG=1): the
+// pre-filter also requires the diagonal circle pixels {2, 6, 10, 14} to hold an adjacent
+// pair (n < 12) or three of four (n >= 12) of the same polarity -- exact, a necessary
+// condition like the cardinal test.
+#ifndef FDF_DIAG
+#define FDF_DIAG 0
+#endif
+constexpr bool kDiagPrefilter = FDF_DIAG != 0;
 
 // Rows of keypoint bitmap above and below a band: NMS compares a band's edge rows with the
 // neighbouring bands' rows, so the band also tests one row each side (scores only).
@@ -174,7 +182,24 @@ struct BandParams {
     uint32_t tasks_per_group;
     uint32_t* kp_stats;          // NMS: += each band's keypoints before suppression (NULL: off)
     uint64_t* stamps;            // debug builds: kStampWords per workgroup (NULL: off)
+    // Direct output (small grids, every workgroup resident at once): each band finds its
+    // output position by a decoupled look-back over the bands before it and writes its points
+    // to `out` itself; no compaction launch.  The band slots are still written (a host call
+    // whose output has to grow runs compact_kernel from them).
+    uint32_t direct;             // 1: direct output
+    uint32_t epoch;              // this launch's tag in the look-back descriptors
+    uint64_t* lookback;          // ntasks descriptors: epoch << 32 | kLbAggregate / kLbPrefix | value
+    uint2* out;                  // direct: the caller's points, `cap` of them
+    uint64_t cap;
+    uint64_t* frame_offsets;     // direct: frames + 1 entries
 };
+constexpr uint64_t kLbAggregate = 1ull << 30;   // value = the band's own keypoint count
+constexpr uint64_t kLbPrefix = 1ull << 31;      // value = keypoints of bands 0 .. this one
+constexpr uint64_t kLbValue = kLbAggregate - 1;
+// Direct output only when the whole grid is resident at once (look-back waits on earlier
+// bands only, and they must already be running): up to this many workgroups, within
+// the CU count times the workgroups one CU holds (host side, fdf_api.cpp).
+constexpr uint32_t kDirectMaxTasks = 1024;
 
 hipError_t launch_compact(const CompactParams& c, hipStream_t stream);
 hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);

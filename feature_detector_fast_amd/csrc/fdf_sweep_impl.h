@@ -60,13 +60,14 @@ template <int LC> struct LaneRow;
 template <> struct LaneRow<16> { using type = u32x4; };
 template <> struct LaneRow<8> { using type = u32x2; };
 
-// DPP whole-wave shifts (GFX9 encodings): lane i reads lane i+1 / lane i-1; the lane that
-// falls off the wave reads 0 (it is a halo lane whose results are never used).
+// DPP whole-wave shifts (GFX9 encodings): lane i reads lane i+1 / lane i-1.  The lane that
+// falls off the wave (63 / 0) is a halo lane whose results are never used, so its value is
+// left undefined: no `old` operand to initialise (one v_mov per shift, 3 a sweep step).
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
-    return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, false);   // wave_shl:1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, false);   // wave_shl:1
 }
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
-    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, false);   // wave_shr:1
 }
 
 struct RowSource {
@@ -599,6 +600,13 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
+    // kDiagPrefilter: NW / NE flags of row r (pixels (x-2, r-2) and (x+2, r-2)), made from the
+    // diagonal comparisons of row r-2, in slot (r - ys) & 1
+    RowFlags<LC> DNW[2], DNE[2];
+    if constexpr (kDiagPrefilter) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) DNW[q].b = DNW[q].nd = DNE[q].b = DNE[q].nd = (RowV)(0u);
+    }
 
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
     // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
@@ -621,6 +629,43 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
             const RowFlags<LC>& vs = V[(J) & 3];                                             \
             const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
+            RowV dgb = (RowV)(~0u), dgnd = (RowV)(0u);                                       \
+            if constexpr (kDiagPrefilter) {                                                  \
+                /* row yv+2 at columns x+2 and x-2 against the centre row: SE and SW of */   \
+                /* row yv, and (polarity swapped) NW and NE of row yv+2 at x+2 / x-2 */     \
+                const RowV r2 = Rw[((J) + 2) % K];                                           \
+                RowV dp, dq;                                                                 \
+                _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) dp[m] = alignbyte(r2[m + 1], r2[m], 2); \
+                dp[M - 1] = alignbyte(from_next_lane(r2[0]), r2[M - 1], 2);                  \
+                dq[0] = alignbyte(r2[0], from_prev_lane(r2[M - 1]), 2);                      \
+                _Pragma("unroll") for (int m = 1; m < M; ++m) dq[m] = alignbyte(r2[m], r2[m - 1], 2); \
+                const RowFlags<LC> A = compare_rows<LC>(dp, nc, lk);                         \
+                const RowFlags<LC> B = compare_rows<LC>(dq, nc, lk);                         \
+                const RowFlags<LC>& nw = DNW[(J) & 1];                                       \
+                const RowFlags<LC>& ne = DNE[(J) & 1];                                       \
+                _Pragma("unroll") for (int m = 0; m < M; ++m) {                              \
+                    const uint32_t a = ne.b[m], b2 = A.b[m], c2 = B.b[m], d = nw.b[m];      \
+                    const uint32_t ea = ne.nd[m], eb = A.nd[m], ec = B.nd[m], ed = nw.nd[m]; \
+                    /* adjacent diagonals: (NE,SE) (SE,SW) (SW,NW) (NW,NE) */                \
+                    if constexpr (N < 12) {                                                  \
+                        dgb[m] = (a | c2) & (b2 | d);                                        \
+                        dgnd[m] = (ea & ec) | (eb & ed);                                     \
+                    } else {                                                                 \
+                        dgb[m] = (a & c2 & (b2 | d)) | (b2 & d & (a | c2));                  \
+                        dgnd[m] = (ea & ec) | (eb & ed) | ((ea | ec) & (eb | ed));           \
+                    }                                                                        \
+                }                                                                            \
+                /* NW of row yv+2 at x+2: bright = NOT A.nd(x), not-dark = NOT A.b(x); */    \
+                /* NE of row yv+2 at x-2: the same from B(x) */                              \
+                const uint32_t pa = from_prev_lane(A.b[M - 1]), pn = from_prev_lane(A.nd[M - 1]); \
+                const uint32_t qa = from_next_lane(B.b[0]), qn = from_next_lane(B.nd[0]);    \
+                _Pragma("unroll") for (int m = 0; m < M; ++m) {                              \
+                    DNW[(J) & 1].b[m] = ~alignbyte(A.nd[m], m ? A.nd[m - 1] : pn, 2);        \
+                    DNW[(J) & 1].nd[m] = ~alignbyte(A.b[m], m ? A.b[m - 1] : pa, 2);         \
+                    DNE[(J) & 1].b[m] = ~alignbyte(m + 1 < M ? B.nd[m + 1] : qn, B.nd[m], 2); \
+                    DNE[(J) & 1].nd[m] = ~alignbyte(m + 1 < M ? B.b[m + 1] : qa, B.b[m], 2); \
+                }                                                                            \
+            }                                                                                \
             _Pragma("unroll") for (int m = 0; m < M; ++m) {                                  \
                 const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);              \
                 const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);          \
@@ -633,6 +678,10 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 } else {                                                                     \
                     br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
                     nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
+                }                                                                            \
+                if constexpr (kDiagPrefilter) {                                              \
+                    br &= dgb[m];                                                            \
+                    nd |= dgnd[m];                                                           \
                 }                                                                            \
                 cand[m] = br | ~nd;                                                          \
             }                                                                                \
@@ -1012,6 +1061,58 @@ __device__ void band_nms_dense(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
     __syncthreads();
 }
 
+// Direct output (BandParams::direct): the band's first output index -- the keypoints of all
+// bands before it -- by a decoupled look-back.  The band publishes its own count (aggregate)
+// at once, then wave 0 reads the descriptors of the 64 bands before it in one load per lane
+// (agent-scope relaxed atomics: sc1 loads and stores, each descriptor one 8-byte word, so a
+// flag and its value can never be seen apart), sums the aggregates down to the nearest band
+// that has published its inclusive prefix, and publishes its own prefix.  Bands only wait
+// for earlier bands, and the host enables this only when the whole grid is resident, so
+// every wait ends; a wait is still bounded (it never takes more than a few microseconds;
+// the bound only keeps a broken grid from hanging the GPU).  Returns the base in every thread.
+__device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t total,
+                                  uint64_t* s_base) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint64_t ep = (uint64_t)P.epoch << 32;
+    if (tid == 0)
+        __hip_atomic_store(&P.lookback[task], ep | kLbAggregate | total, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 64) {
+        uint64_t excl = 0;
+        int64_t j = (int64_t)task - 1;
+        uint32_t polls = 0;
+        while (j >= 0) {
+            const int64_t k = j - (int64_t)lane;
+            // bands before band 0 read as an inclusive prefix of 0
+            const uint64_t d = k >= 0 ? __hip_atomic_load(&P.lookback[k], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : (ep | kLbPrefix);
+            const bool ok = (d >> 32) == P.epoch && (d & (kLbAggregate | kLbPrefix)) != 0;
+            const uint64_t pref = wave_ballot(ok && (d & kLbPrefix));
+            const uint32_t stop = pref ? (uint32_t)__builtin_ctzll(pref) : 63u;
+            const uint64_t need = stop == 63u ? ~0ull : (2ull << stop) - 1ull;
+            if ((wave_ballot(ok) & need) != need) {
+                if (++polls > (1u << 20)) break;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint64_t v = lane <= stop ? (d & kLbValue) : 0ull;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            excl += v;
+            if (pref) break;
+            j -= 64;
+        }
+        if (lane == 0) {
+            __hip_atomic_store(&P.lookback[task], ep | kLbPrefix | ((excl + total) & kLbValue),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *s_base = excl;
+        }
+    }
+    __syncthreads();
+    return *s_base;
+}
+
 // The band (task) a workgroup sweeps.  XCD-aware static task mapping: each XCD takes a contiguous range of bands (raster
     // order), so consecutive bands of a frame land on one XCD (its L2 then serves the halo
     // rows two neighbouring bands share).  Within its range an XCD dispatches the frames'
@@ -1056,7 +1157,13 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
 
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem_raw + L.bitmap);
     uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.misc);
-    if (P.threshold >= 255) return 0;                                // no pixel can pass
+    if (P.threshold >= 255) {                                        // no pixel can pass
+        if (P.direct && tid == 0) {
+            if (band == 0) P.frame_offsets[frame] = 0;
+            if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = 0;
+        }
+        return 0;
+    }
     uint32_t* unit_ctr = wave_sum + kWaves;
     // the bitmap and its pad word, cleared 16 bytes per store up to the (16-byte aligned)
     // end of its LDS area
@@ -1188,7 +1295,16 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     }
     if (ablation_flags(P.flags) & kFlagNoEmit) return total;
     uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
-    if (total <= P.slot_bytes / 8) {
+    const bool listed = total <= P.slot_bytes / 8;
+    uint64_t dbase = 0;
+    if (P.direct) {
+        dbase = band_lookback(P, task, total, reinterpret_cast<uint64_t*>(smem_raw + L.misc + 32));
+        if (tid == 0) {
+            if (band == 0) P.frame_offsets[frame] = dbase;
+            if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = dbase + total;
+        }
+    }
+    if (listed || P.direct) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
         uint32_t o = before;
         for (uint32_t w0 = wb; w0 < we; w0 += 64) {
@@ -1203,10 +1319,14 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
             while (bits) {
                 const uint32_t bit = __builtin_ctz(bits);
                 bits &= bits - 1;
-                pts[idx++] = make_uint2(xb + bit, y0 + r);
+                const uint2 pt = make_uint2(xb + bit, y0 + r);
+                if (listed) pts[idx] = pt;
+                if (P.direct && dbase + idx < P.cap) P.out[dbase + idx] = pt;
+                ++idx;
             }
         }
-    } else {
+    }
+    if (!listed) {
         uint32_t* words = reinterpret_cast<uint32_t*>(slot);
         for (uint32_t w = tid; w < nwords; w += kThreads) words[w] = keep[w];
     }

@@ -50,11 +50,29 @@ def test_crate_api_returns_points(golden):
     assert Config(16, 9).detect(gi) == pts
 
 
+@pytest.fixture(scope="module")
+def compare_input(golden):
+    """The image of tests/compare.rs: $INPUT_FILE when set (any PNG/PGM: opened as RGB8 and
+    converted with image 0.24.6's to_luma8, compare.rs:24-33), else the reference's test image
+    (the golden fixture, already grey)."""
+    path = os.environ.get("INPUT_FILE")
+    if not path:
+        return golden[0], None
+    return workloads.input_image(path)
+
+
 @pytest.mark.parametrize("t,n,nms", [(16, 9, 0), (16, 9, 1), (16, 9, 2), (16, 12, 2),
                                      (32, 12, 2)])
-def test_compare_rs_configs(golden, t, n, nms):
-    """tests/compare.rs:66-114: the five configurations of the reference's parity test."""
-    assert_same(golden[0], t, n, nms)
+def test_compare_rs_configs(compare_input, t, n, nms):
+    """tests/compare.rs:66-114: the five configurations of the reference's parity test, on
+    $INPUT_FILE when set.  With max-t, the reference's hash guard (compare.rs:83-89): on its
+    own test image (RGB bytes hashing to 0x8444a9356505ecab) the keypoints must hash to
+    0x8bf9cd0f9ca9ebec (Rust's DefaultHasher, workloads.rust_hash_points)."""
+    img, rgb = compare_input
+    assert_same(img, t, n, nms)
+    if nms == 1 and rgb is not None:
+        if workloads.rust_hash_bytes(rgb) == workloads.REF_IMAGE_HASH:
+            assert workloads.rust_hash_points(run(img, t, n, nms)) == workloads.REF_MAXT_HASH
 
 
 def test_hand_kat():

@@ -422,3 +422,37 @@ def test_byte_broadcast_and_partial_entry_mask():
         new = m & ((~0 << (last + 1)) & 0xffffffff)
         old = m & ((~0 << select_bit(m, taken)) & 0xffffffff)
         assert new == old
+
+
+def test_rust_default_hasher():
+    """workloads.siphash: SipHash-2-4's published vectors (key 00..0f; messages of 0 and 15
+    bytes), so the SipHash-1-3 of Rust's DefaultHasher (tests/compare.rs:5-20 hash guard)
+    runs the same code with fewer rounds; and the byte stream `Hash` writes for &[u8] and
+    &[Point] (length as a LE usize, then the elements)."""
+    k0 = int.from_bytes(bytes(range(8)), "little")
+    k1 = int.from_bytes(bytes(range(8, 16)), "little")
+    assert workloads.siphash(b"", 2, 4, k0, k1) == 0x726FDB47DD0E0E31
+    assert workloads.siphash(bytes(range(15)), 2, 4, k0, k1) == 0xA129CA6149BE45E5
+    pts = np.array([[3, 4], [70000, 5]], dtype=np.uint32)
+    stream = (2).to_bytes(8, "little") + b"".join(int(v).to_bytes(4, "little") for v in pts.reshape(-1))
+    assert workloads.rust_hash_points(pts) == workloads.siphash(stream)
+    assert workloads.rust_hash_bytes(b"\x01\x02") == workloads.siphash((2).to_bytes(8, "little") + b"\x01\x02")
+
+
+def test_input_image_is_compare_rs_luma(tmp_path):
+    """An INPUT_FILE goes through to_rgb8 and to_luma8 as tests/compare.rs:29-33 does: the
+    golden grey fixture written as PNG comes back unchanged (r = g = b), and a colour PNG
+    gives image 0.24.6's integer luma."""
+    from PIL import Image
+
+    g = workloads.golden_image()
+    p = tmp_path / "grey.png"
+    Image.fromarray(g).save(p)
+    grey, rgb = workloads.input_image(str(p))
+    assert np.array_equal(grey, g) and rgb.shape == g.shape + (3,)
+    rng = np.random.default_rng(5)
+    col = rng.integers(0, 256, (20, 30, 3), dtype=np.uint8)
+    p2 = tmp_path / "col.png"
+    Image.fromarray(col).save(p2)
+    grey2, _ = workloads.input_image(str(p2))
+    assert np.array_equal(grey2, oracle.rgb_to_luma(col))

@@ -2,7 +2,8 @@
 # One GPU lease, many steps: tools/lease.sh OUT STEP [STEP ...]   (outputs under gpurun_out/OUT)
 # Every step runs under its own time limit; the first failing step ends the lease (no retries).
 # A STEP is "kind|arg|arg...":
-#   tests[|-k EXPR]                    pytest -m gpu (all GPU tests, or those matching EXPR)
+#   tests[|EXPR]                       pytest -m gpu (all GPU tests, or those matching -k EXPR)
+#   testslib|LIB|EXPR                  the same on another build of the library (FDF_LIB_PATH)
 #   smoke                              __graft_entry__.smoke()
 #   bench|NAME|ARGS                    python bench.py ARGS            -> NAME.json
 #   ab|NAME|ROUNDS|VARIANTS|ARGS|LIBS  interleaved A/B of library builds (LIBS comma-separated,
@@ -30,6 +31,9 @@ for STEP in "$@"; do
       K=()
       [ -n "$A1" ] && K=(-k "$A1")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${K[@]}" > "$L" 2>&1 || fail "$STEP" "$L"
+      tail -2 "$L" ;;
+    testslib)
+      FDF_LIB_PATH=$A1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$A2" > "$L" 2>&1 || fail "$STEP" "$L"
       tail -2 "$L" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$L" 2>&1 || fail "$STEP" "$L"

@@ -157,7 +157,8 @@ def siphash(data, c_rounds=1, d_rounds=3, k0=0, k1=0):
 
 def rust_hash_bytes(buf):
     """`DefaultHasher` of a &[u8] (compare.rs:13-20 hash_slice_u8)."""
-    b = np.ascontiguousarray(buf, dtype=np.uint8).tobytes()
+    b = bytes(buf) if isinstance(buf, (bytes, bytearray)) else \
+        np.ascontiguousarray(buf, dtype=np.uint8).tobytes()
     return siphash(len(b).to_bytes(8, "little") + b)
 
 
