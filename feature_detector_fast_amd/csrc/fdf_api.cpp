@@ -75,7 +75,6 @@ struct fdf_ctx {
     std::vector<hipEvent_t> ev;           // 3 per recorded call, kMaxTimedCalls at most
     // direct output of small grids (BandParams::direct): look-back descriptors, launch tag
     uint64_t* d_lookback = nullptr;       size_t lookback_n = 0;
-    uint32_t epoch = 0;
     uint32_t cus = 0;                     // compute units of the device
     // debug builds (FDF_STAMPS set): the last detector launch's workgroup stamps
     uint64_t* d_stamps = nullptr;         size_t stamps_n = 0;
@@ -84,6 +83,10 @@ struct fdf_ctx {
 
 constexpr size_t kMaxTimedCalls = 4096;
 constexpr uint64_t kDefaultMinTasks = 1024;   // 4 workgroups on each of 256 CUs
+
+// process-wide counters: fdf_detect_batch_multi call generations, direct-output launch tags
+std::atomic<uint64_t> g_multi_gen{0};
+std::atomic<uint32_t> g_launch_epoch{0};
 
 namespace {
 
@@ -203,7 +206,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
         if (eff > best + 1e-9) { best = eff; g.R = R; }
     }
     if (g.R == 0) {
-        const uint32_t unit = fdfk::kSweepRing - 3 - halo;
+        const uint32_t unit = fdfk::kSweepRing - halo;
         g.R = g.nsub * unit;
         while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, nms).total > budget)
             g.R -= g.nsub;
@@ -346,13 +349,17 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.cap = cap;
     p.frame_offsets = d_offsets;
     if (direct) {
-        uint64_t* prev = ctx->d_lookback;
+        // a (re)allocated buffer is zeroed: recycled device memory can hold descriptors of
+        // another context's launches.  Launch tags are unique in the process as well.
+        const size_t had = ctx->lookback_n;
         if ((rc = ensure(ctx, &ctx->d_lookback, &ctx->lookback_n, (size_t)ntasks, stream))) return rc;
-        if (ctx->d_lookback != prev &&   // a new buffer: no stale launch tags
+        if (ctx->lookback_n != had &&
             hipMemsetAsync(ctx->d_lookback, 0, ctx->lookback_n * sizeof(uint64_t), stream) != hipSuccess)
             return FDF_ERR_DEVICE;
         p.lookback = ctx->d_lookback;
-        p.epoch = ++ctx->epoch == 0 ? ++ctx->epoch : ctx->epoch;   // fresh buffers read as 0
+        uint32_t e = ++g_launch_epoch;
+        if (e == 0) e = ++g_launch_epoch;                          // 0 = a zeroed descriptor
+        p.epoch = e;
     }
 #ifdef FDF_DEBUG_BUILD
     if (std::getenv("FDF_STAMPS")) {
@@ -587,7 +594,6 @@ std::vector<std::unique_lock<std::mutex>> lock_all(fdf_ctx* const* ctxs, uint32_
     return locks;
 }
 
-std::atomic<uint64_t> g_multi_gen{0};
 
 // Copy of the last host result (fdf_fetch_last), lock held.
 int fetch_last(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t cap, size_t* n_out) {

@@ -121,10 +121,10 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     return L;
 }
 
-// Sweep steps of a unit of `rows` owned rows plus `halo` extra tested rows: 3 rows of
-// vertical look-ahead, in whole kSweepRing-step blocks.
+// Sweep steps of a unit of `rows` owned rows plus `halo` extra tested rows, in whole
+// kSweepRing-step blocks (the 3 rows of vertical look-ahead are a prologue, not steps).
 __host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t halo) {
-    return (rows + halo + 3 + kSweepRing - 1) / kSweepRing * kSweepRing;
+    return (rows + halo + kSweepRing - 1) / kSweepRing * kSweepRing;
 }
 
 __host__ __device__ inline uint32_t align16(uint32_t v) { return (v + 15u) & ~15u; }

@@ -577,7 +577,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         }
     }
     const int p0 = u.p0, p1 = u.p1;                    // rows run through the pre-filter
-    const int ys = p0 - 3;                             // first row of vertical comparisons
+    const int ys = p0;                                 // first swept row
     u.ys = ys;
     u.rowbase = (ys - 3) * W;
     const int T = p1 - ys;                             // sweep steps (row ys + i at step i)
@@ -597,9 +597,18 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     // register move.  The loop body is K steps, so unit sweeps are whole multiples of K.
     constexpr int K = kSweepRing;
     RowV Rw[K];
+    // The N flags of rows p0 .. p0+2 come from the vertical comparisons of rows p0-3 .. p0-1
+    // with them, which the steps of those rows would have made: a prologue makes only those
+    // three comparisons (3 loads and 48 lerps instead of three whole pre-filter steps whose
+    // candidates are masked)
+    RowV up[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) up[k] = load_row<LC, EXACT>(u.src, ys - 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
+#pragma unroll
+    for (int k = 0; k < 3; ++k) V[k + 1] = compare_rows<LC>(Rw[k], ~up[k], lk);
     // kDiagPrefilter: NW / NE flags of row r (pixels (x-2, r-2) and (x+2, r-2)), made from the
     // diagonal comparisons of row r-2, in slot (r - ys) & 1
     RowFlags<LC> DNW[2], DNE[2];

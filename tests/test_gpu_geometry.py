@@ -110,3 +110,50 @@ def test_config5_batch_repeated():
     for f in sorted({0, *dens.tolist()}):
         want = oracle.detect(batch[f].cpu().numpy(), 8, 12, 2)
         assert np.array_equal(p[o[f]:o[f + 1]], want), f
+
+
+@pytest.mark.parametrize("nms", [0, 1, 2])
+def test_direct_output_batches(nms):
+    """Grids small enough to be resident at once write their points directly (each band's
+    output index from a decoupled look-back over the bands before it, no compaction launch):
+    an 8-frame 1080p batch (~860 bands) mixing S1, S2 and dense S3 frames, launched 5 times
+    on the device path -- every launch equals the first, and every frame equals the oracle."""
+    import torch
+
+    host = [workloads.s1_frame(3), workloads.s3_frame(6), workloads.s2_frame(2), workloads.s1_frame(11),
+            workloads.s3_frame(7), workloads.s1_frame(20), workloads.s2_frame(5), workloads.s1_frame(0)]
+    frames = torch.from_numpy(np.stack(host)).cuda()
+    cfg = Config(16, 9, NonMaximalSuppression(nms))
+    out = torch.empty((8 * 700_000, 2), dtype=torch.int32, device="cuda")
+    offs = torch.zeros(9, dtype=torch.int64, device="cuda")
+    runs = []
+    for _ in range(5):
+        out.fill_(-1)
+        fast_hip.detect_device(frames, cfg, out, offs)
+        torch.cuda.synchronize()
+        o = offs.cpu().numpy().copy()
+        runs.append((o, out[: o[-1]].cpu().numpy().astype(np.uint32)))
+    for o, p in runs[1:]:
+        assert np.array_equal(o, runs[0][0]) and np.array_equal(p, runs[0][1])
+    o, p = runs[0]
+    for f in range(8):
+        assert np.array_equal(p[o[f]:o[f + 1]], oracle.detect(host[f], 16, 9, nms)), f
+
+
+def test_direct_output_4k_frame_and_capacity():
+    """One 4K frame (~430 bands at the single-frame geometry) through the direct path with
+    the output capacity short of the total: the first `cap` points are written, offsets hold
+    the full total, and the host API's two-call pattern returns the whole oracle list."""
+    import torch
+
+    img = workloads.s1_frame(4, 3840, 2160)
+    want = oracle.detect(img, 8, 12, 0)
+    frames = torch.from_numpy(img).cuda().unsqueeze(0).contiguous()
+    cap = len(want) // 2
+    out = torch.full((cap, 2), -1, dtype=torch.int32, device="cuda")
+    offs = torch.zeros(2, dtype=torch.int64, device="cuda")
+    fast_hip.detect_device(frames, Config(8, 12, NonMaximalSuppression.Off), out, offs)
+    torch.cuda.synchronize()
+    assert int(offs[1]) == len(want) and int(offs[0]) == 0
+    assert np.array_equal(out.cpu().numpy().astype(np.uint32), want[:cap])
+    assert np.array_equal(fast_hip.detect_array(img, Config(8, 12, NonMaximalSuppression.Off)), want)
