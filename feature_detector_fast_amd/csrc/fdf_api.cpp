@@ -154,7 +154,7 @@ struct Geometry {
 
 
 Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
-                       uint64_t min_tasks, double density, uint32_t forced_rows) {
+                       uint64_t slots, double density, uint32_t forced_rows) {
     Geometry g;
     const uint32_t sc = (uint32_t)fdfk::strip_cols(fdfk::kLaneCols);
     g.nstrips = (w - 3 + sc - 1) / sc;
@@ -176,11 +176,16 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     if (const char* b = std::getenv("FDF_LDS_BUDGET"))
         budget = std::min<uint32_t>(fdfk::kSweepMaxLds, (uint32_t)std::strtoul(b, nullptr, 0));
 #endif
-    // Among band heights whose grid fills the chip (>= min_tasks workgroups), take the one
-    // with the most owned rows per sweep step; a grid that cannot fill the chip takes the
-    // shortest sweep (one ring block per unit) for the lowest latency.  min_tasks = 1
-    // (fdf_ctx_set_geometry, tests) gives a small job the full-size geometry (tall bands,
-    // long units); the keypoints are the same either way.
+    // The band height with the shortest modelled launch (in sweep-step units): every unit
+    // costs its steps plus kUnitCost (prologue, flush, unit hand-out), every workgroup
+    // kBandCost more (LDS clear, NMS pass, emit), and the grid runs on `slots` workgroup
+    // slots at once -- time = max(total / slots, one workgroup) + half a workgroup of tail
+    // (workgroups of one height differ with their rows' content, up to ~1.5x).  So a grid
+    // that cannot fill the chip takes the shortest bands (lowest latency), a large batch
+    // the tallest that waste no padding steps, and a grid near one round of the chip neither
+    // spills into a second round nor leaves slots idle.  slots = 1 (fdf_ctx_set_geometry,
+    // tests) gives a small job the full-size geometry (tall bands, long units); the
+    // keypoints are the same either way.
     // NMS: when an earlier launch of this configuration measured the keypoint density, keep
     // a band's expected keypoints (x1.5) within the LDS score list, so that bands do not
     // spill (4K t=8 n=12 SAD: 27-row bands instead of 43, 0.747 -> 0.732 ms)
@@ -195,22 +200,27 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
             g.R -= g.nsub;
         return g;
     }
-    double best = -1.0;
+    constexpr double kUnitCost = 3.0;
+    const double band_cost = nms ? 4.0 : 2.0;
+    const uint32_t units_per_wave = (g.nstrips * g.nsub + fdfk::kWaves - 1) / fdfk::kWaves;
+    auto wg_cost = [&](uint32_t rows) {
+        const uint32_t unit_rows = (rows + g.nsub - 1) / g.nsub;
+        return units_per_wave * ((double)fdfk::sweep_steps(unit_rows, halo) + kUnitCost) + band_cost;
+    };
+    double best = 0.0;
     g.R = 0;
     for (uint32_t R = g.nsub; R <= max_rows && R < centre_rows + g.nsub; R += g.nsub) {
         if (fdfk::make_sweep_layout(R, nw, nms).total > budget) break;
-        const uint64_t tasks = (uint64_t)n_frames * ((centre_rows + R - 1) / R);
-        if (tasks < min_tasks) break;
-        const uint32_t steps = fdfk::sweep_steps(R / g.nsub, halo);
-        const double eff = (double)R / (double)(steps * g.nsub);
-        if (eff > best + 1e-9) { best = eff; g.R = R; }
+        const uint32_t bands = (centre_rows + R - 1) / R;
+        const double full = wg_cost(R), last = wg_cost(centre_rows - (bands - 1) * R);
+        const double total = (double)n_frames * ((bands - 1) * full + last);
+        const double t = std::max(total / (double)slots, full) + 0.5 * full;
+        if (g.R == 0 || t <= best * 1.001) {  // ties: the taller band (fewer workgroups)
+            best = t;
+            g.R = R;
+        }
     }
-    if (g.R == 0) {
-        const uint32_t unit = fdfk::kSweepRing - halo;
-        g.R = g.nsub * unit;
-        while (g.R > g.nsub && fdfk::make_sweep_layout(g.R, nw, nms).total > budget)
-            g.R -= g.nsub;
-    }
+    if (g.R == 0) g.R = g.nsub;
     return g;
 }
 
@@ -243,9 +253,11 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
                 density = (double)(uint32_t)v / li.pixels;
         }
     }
-    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms,
-                                       ctx->min_tasks ? ctx->min_tasks : kDefaultMinTasks, density,
-                                       ctx->band_rows);
+    // workgroup slots of the device: 4 per CU (4 waves per SIMD); fdf_ctx_set_geometry's
+    // min_tasks replaces it (1: the tall bands of a large batch for any job)
+    const uint64_t slots = ctx->min_tasks ? ctx->min_tasks
+                                          : (ctx->cus ? 4ull * ctx->cus : kDefaultMinTasks);
+    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
     if (fdfk::make_sweep_layout(R, nw, cfg->nms).total > fdfk::kSweepMaxLds)

@@ -35,8 +35,10 @@ constexpr bool kDebugBuild = false;
 #endif
 // Debug builds: per-workgroup stamps of the detector (BandParams::stamps, kStampWords words per
 // workgroup): shader clock and 100 MHz real time at the workgroup's start and end, its XCD
-// and hardware id, its band.  Written only to that buffer; no output depends on them.
-constexpr uint32_t kStampWords = 6;
+// and hardware id, its band, and the shader clock at the end of its phases as wave 0 sees
+// them (setup, its sweep, NMS, look-back).  Written only to that buffer; no output depends
+// on them.
+constexpr uint32_t kStampWords = 10;
 
 // Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).
@@ -67,14 +69,6 @@ constexpr int kSweepRing = FDF_RING;
 #define FDF_WAVES_PER_EU 4
 #endif
 constexpr int kSweepWavesPerEU = FDF_WAVES_PER_EU;
-// A/B variant (built by tools/build_variant.sh with -DFDF_DIAG=1): the
-// pre-filter also requires the diagonal circle pixels {2, 6, 10, 14} to hold an adjacent
-// pair (n < 12) or three of four (n >= 12) of the same polarity -- exact, a necessary
-// condition like the cardinal test.
-#ifndef FDF_DIAG
-#define FDF_DIAG 0
-#endif
-constexpr bool kDiagPrefilter = FDF_DIAG != 0;
 
 // Rows of keypoint bitmap above and below a band: NMS compares a band's edge rows with the
 // neighbouring bands' rows, so the band also tests one row each side (scores only).

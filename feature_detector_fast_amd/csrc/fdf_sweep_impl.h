@@ -609,14 +609,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 #pragma unroll
     for (int k = 0; k < 3; ++k) V[k + 1] = compare_rows<LC>(Rw[k], ~up[k], lk);
-    // kDiagPrefilter: NW / NE flags of row r (pixels (x-2, r-2) and (x+2, r-2)), made from the
-    // diagonal comparisons of row r-2, in slot (r - ys) & 1
-    RowFlags<LC> DNW[2], DNE[2];
-    if constexpr (kDiagPrefilter) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) DNW[q].b = DNW[q].nd = DNE[q].b = DNE[q].nd = (RowV)(0u);
-    }
-
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
     // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
     // their candidates masked: a branch around it costs the zeroing of `cand` on every step.
@@ -638,43 +630,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
             const RowFlags<LC>& vs = V[(J) & 3];                                             \
             const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
-            RowV dgb = (RowV)(~0u), dgnd = (RowV)(0u);                                       \
-            if constexpr (kDiagPrefilter) {                                                  \
-                /* row yv+2 at columns x+2 and x-2 against the centre row: SE and SW of */   \
-                /* row yv, and (polarity swapped) NW and NE of row yv+2 at x+2 / x-2 */     \
-                const RowV r2 = Rw[((J) + 2) % K];                                           \
-                RowV dp, dq;                                                                 \
-                _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) dp[m] = alignbyte(r2[m + 1], r2[m], 2); \
-                dp[M - 1] = alignbyte(from_next_lane(r2[0]), r2[M - 1], 2);                  \
-                dq[0] = alignbyte(r2[0], from_prev_lane(r2[M - 1]), 2);                      \
-                _Pragma("unroll") for (int m = 1; m < M; ++m) dq[m] = alignbyte(r2[m], r2[m - 1], 2); \
-                const RowFlags<LC> A = compare_rows<LC>(dp, nc, lk);                         \
-                const RowFlags<LC> B = compare_rows<LC>(dq, nc, lk);                         \
-                const RowFlags<LC>& nw = DNW[(J) & 1];                                       \
-                const RowFlags<LC>& ne = DNE[(J) & 1];                                       \
-                _Pragma("unroll") for (int m = 0; m < M; ++m) {                              \
-                    const uint32_t a = ne.b[m], b2 = A.b[m], c2 = B.b[m], d = nw.b[m];      \
-                    const uint32_t ea = ne.nd[m], eb = A.nd[m], ec = B.nd[m], ed = nw.nd[m]; \
-                    /* adjacent diagonals: (NE,SE) (SE,SW) (SW,NW) (NW,NE) */                \
-                    if constexpr (N < 12) {                                                  \
-                        dgb[m] = (a | c2) & (b2 | d);                                        \
-                        dgnd[m] = (ea & ec) | (eb & ed);                                     \
-                    } else {                                                                 \
-                        dgb[m] = (a & c2 & (b2 | d)) | (b2 & d & (a | c2));                  \
-                        dgnd[m] = (ea & ec) | (eb & ed) | ((ea | ec) & (eb | ed));           \
-                    }                                                                        \
-                }                                                                            \
-                /* NW of row yv+2 at x+2: bright = NOT A.nd(x), not-dark = NOT A.b(x); */    \
-                /* NE of row yv+2 at x-2: the same from B(x) */                              \
-                const uint32_t pa = from_prev_lane(A.b[M - 1]), pn = from_prev_lane(A.nd[M - 1]); \
-                const uint32_t qa = from_next_lane(B.b[0]), qn = from_next_lane(B.nd[0]);    \
-                _Pragma("unroll") for (int m = 0; m < M; ++m) {                              \
-                    DNW[(J) & 1].b[m] = ~alignbyte(A.nd[m], m ? A.nd[m - 1] : pn, 2);        \
-                    DNW[(J) & 1].nd[m] = ~alignbyte(A.b[m], m ? A.b[m - 1] : pa, 2);         \
-                    DNE[(J) & 1].b[m] = ~alignbyte(m + 1 < M ? B.nd[m + 1] : qn, B.nd[m], 2); \
-                    DNE[(J) & 1].nd[m] = ~alignbyte(m + 1 < M ? B.b[m + 1] : qa, B.b[m], 2); \
-                }                                                                            \
-            }                                                                                \
             _Pragma("unroll") for (int m = 0; m < M; ++m) {                                  \
                 const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);              \
                 const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);          \
@@ -687,10 +642,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 } else {                                                                     \
                     br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
                     nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
-                }                                                                            \
-                if constexpr (kDiagPrefilter) {                                              \
-                    br &= dgb[m];                                                            \
-                    nd |= dgnd[m];                                                           \
                 }                                                                            \
                 cand[m] = br | ~nd;                                                          \
             }                                                                                \
@@ -1151,7 +1102,8 @@ __device__ __forceinline__ uint32_t band_task(const BandParams& P) {
 
 // Sweeps band `task`, runs its NMS and writes its slot; returns the band's keypoint count.
 template <int NMS, int N>
-__device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* smem_raw, uint32_t task) {
+__device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* smem_raw, uint32_t task,
+                                              uint64_t (&ph)[4]) {
     constexpr int LC = kLaneCols;
     const SweepLayout L = make_sweep_layout(P.rows, P.words_per_row, NMS);
     const uint32_t tid = threadIdx.x;
@@ -1183,6 +1135,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         unit_ctr[1] = 0;
     }
     __syncthreads();
+    if constexpr (kDebugBuild) ph[0] = __builtin_amdgcn_s_memtime();   // setup done
 
     SweepShared sh;
     sh.pq = reinterpret_cast<uint32_t*>(smem_raw + L.pq + wave * L.wave_bytes);
@@ -1249,6 +1202,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         if constexpr (NMS == kNmsMaxThreshold)
             if (u.kq_n != 0) score_kp_queue<N>(sh, u, u.kq_n);
     }
+    if constexpr (kDebugBuild) ph[1] = __builtin_amdgcn_s_memtime();   // this wave's sweep done
     __syncthreads();
 
     const uint32_t nwords = rows * nw;
@@ -1283,6 +1237,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         // the band's own rows are now its keep-bits
     }
     const uint32_t* keep = bitmap + halo * nw;
+    if constexpr (kDebugBuild) ph[2] = __builtin_amdgcn_s_memtime();   // NMS done
 
     // ---- count keep-bits and write the band slot
     // Each wave owns a contiguous quarter of the bitmap and sweeps it 64 words per round (lane
@@ -1308,6 +1263,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     uint64_t dbase = 0;
     if (P.direct) {
         dbase = band_lookback(P, task, total, reinterpret_cast<uint64_t*>(smem_raw + L.misc + 32));
+        if constexpr (kDebugBuild) ph[3] = __builtin_amdgcn_s_memtime();   // look-back done
         if (tid == 0) {
             if (band == 0) P.frame_offsets[frame] = dbase;
             if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = dbase + total;
@@ -1356,7 +1312,8 @@ void fast_sweep_kernel(BandParams P) {
         }
     }
     const uint32_t task = band_task(P);
-    const uint32_t total = sweep_band<NMS, N>(P, smem_raw, task);
+    uint64_t ph[4] = {0, 0, 0, 0};
+    const uint32_t total = sweep_band<NMS, N>(P, smem_raw, task, ph);
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
         P.counts[task] = total;
@@ -1377,6 +1334,7 @@ void fast_sweep_kernel(BandParams P) {
                 s[4] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) |
                        (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
                 s[5] = task;
+                for (int k = 0; k < 4; ++k) s[6 + k] = ph[k];   // phases (wave 0's view)
             }
         }
     }

@@ -38,11 +38,12 @@ def main():
     out = torch.empty((args.frames * 50_000, 2), dtype=torch.int32, device="cuda")
     offs = torch.zeros(args.frames + 1, dtype=torch.int64, device="cuda")
     modes = {"off": 0, "maxt": 1, "sad": 2}
-    # mode:flags[:lds_budget[:nsub]] -- budget (bytes per workgroup) and sub-bands per band
-    # override the geometry pick (0 = default)
+    # mode:flags[:lds_budget[:nsub[:rows]]] -- budget (bytes per workgroup), sub-bands per
+    # band and band rows (fdf_ctx_set_band_rows) override the geometry pick (0 = default)
     variants = [tuple(v.split(":")) for v in args.variants.split(",")]
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream()
+    ctx = fast_hip.context(0)
     for r in range(args.rounds):
         for v in variants:
             mode, flags = v[0], v[1]
@@ -52,6 +53,7 @@ def main():
                     os.environ[name] = v[k]
                 else:
                     os.environ.pop(name, None)
+            ctx.set_band_rows(int(v[4]) if len(v) > 4 else 0)
             cfg = Config(args.threshold, args.count, NonMaximalSuppression(modes[mode]))
             fast_hip.detect_device(frames, cfg, out, offs, stream=stream)
             s = torch.cuda.Event(enable_timing=True)
@@ -63,6 +65,7 @@ def main():
             torch.cuda.synchronize()
             times[v].append(s.elapsed_time(e) / args.iters)
     os.environ.pop("FDF_DEBUG_FLAGS", None)
+    ctx.set_band_rows(0)
     px = args.frames * args.width * args.height
     res = {}
     for v, ts in times.items():

@@ -63,7 +63,7 @@ for STEP in "$@"; do
       rm -rf "$D" ;;
     stamps)
       FDF_LIB_PATH=$DEBUG_LIB timeout -k 10 400 python3 tools/stamps.py $A2 > "$O/$A1.json" 2> "$L" || fail "$STEP" "$L"
-      python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['by_frames']; [print(f, {k: v[k] for k in ('span_us','ramp_us','tail_us_p90_to_last','wg_us_p5_p50_p95','busy_fraction','clock_mhz_p50','event_ms_p50')}) for f, v in d.items()]" "$O/$A1.json" ;;
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['by_frames']; [print(f, {k: v[k] for k in ('span_us','ramp_us','tail_us_p90_to_last','wg_us_p5_p50_p95','busy_fraction','clock_mhz_p50','event_ms_p50','workgroups','phases_cycles_p50')}) for f, v in d.items()]" "$O/$A1.json" ;;
     profile)
       timeout -k 10 900 bash tools/profile_round.sh "$A1" $A2 > "$L" 2>&1 || fail "$STEP" "$L"
       tail -1 "$L" ;;

@@ -21,11 +21,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("FDF_LIB_PATH", os.path.join(ROOT, "build", "libfdf_debug.so"))
 os.environ["FDF_STAMPS"] = "1"
-WORDS = 6
+WORDS = 10
 
 
 def summarize(st, ntasks_expected):
-    t0, t1, r0, r1, ids, task = (st[:, k] for k in range(WORDS))
+    t0, t1, r0, r1, ids, task = (st[:, k] for k in range(6))
+    ph = st[:, 6:10]
     xcc = (ids >> 32) & 0xF
     hw = ids & 0xFFFFFFFF
     cu = (hw >> 8) & 0xF
@@ -48,7 +49,21 @@ def summarize(st, ntasks_expected):
                         "end_us": round(float(e_us[m].max()), 2),
                         "wg_us_mean": round(float(dur[m].mean()), 2)}
     order = np.sort(e_us)
-    return {
+    # phases in shader cycles from the workgroup's start: setup, wave 0's sweep, the rest of
+    # the band's sweep (barrier), NMS, look-back (direct output), emit + end
+    marks = np.concatenate([t0[:, None], np.where(ph > 0, ph, 0), t1[:, None]], axis=1)
+    phases = {}
+    names = ["setup", "sweep_wave0", "sweep_rest_and_nms", "lookback", "emit_end"]
+    prev = marks[:, 0]
+    for k, name in enumerate(names[:-1]):
+        m = marks[:, k + 1]
+        ok = m > 0
+        if ok.any():
+            phases[name] = round(float(np.median((m - prev)[ok])), 0)
+            prev = np.where(ok, m, prev)
+    phases["emit_end"] = round(float(np.median(marks[:, -1] - prev)), 0)
+    phases["total_cycles"] = round(float(np.median(t1 - t0)), 0)
+    return {"phases_cycles_p50": phases,
         "workgroups": int(len(st)), "ntasks": int(ntasks_expected),
         "span_us": round(span, 2),
         "cus_seen": len(first_per_cu),
