@@ -10,6 +10,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <condition_variable>
 #include <mutex>
@@ -57,7 +58,13 @@ struct fdf_ctx {
     uint64_t* d_stats = nullptr;        // its device address
     uint32_t stats_seq = 0;
     struct LaunchInfo { uint32_t seq = 0, t = 0, n = 0, nms = 0, w = 0; double pixels = 0; };
-    LaunchInfo hist[8];
+    LaunchInfo hist[64];
+    // the last density read, kept for its configuration: with more launches in flight than
+    // `hist` holds, a read finds its launch's record overwritten (the band height then
+    // alternated between launches of one configuration)
+    // (one per NMS mode, so that interleaved modes keep theirs)
+    LaunchInfo known[3];
+    double known_density[3] = {0.0, 0.0, 0.0};
     // cross-stream ordering: the device work of the last enqueue (on any stream) completes
     // at `done`; the next enqueue on another stream waits for it first
     hipEvent_t done = nullptr;
@@ -187,11 +194,16 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     // tests) gives a small job the full-size geometry (tall bands, long units); the
     // keypoints are the same either way.
     // NMS: when an earlier launch of this configuration measured the keypoint density, keep
-    // a band's expected keypoints (x1.5) within the LDS score list, so that bands do not
-    // spill (4K t=8 n=12 SAD: 27-row bands instead of 43, 0.747 -> 0.732 ms)
+    // a band's expected keypoints (x1.2) within the LDS score list, so that few bands
+    // spill (4K t=8 n=12 SAD: 38-row bands; margins 1.5 / 1.2 / 1.0 / 0.8 measured 0.726 /
+    // 0.716 / 0.715 / 0.730 ms, profiles/r03/l4_margin_4k.json)
     uint32_t max_rows = 256;
-    if (nms && density > 0.0) {
-        const double rows = (double)fdfk::kScoreListCap / (1.5 * density * (double)w) - 2.0;
+    double margin = 1.2;
+#ifdef FDF_DEBUG_BUILD
+    if (const char* e = std::getenv("FDF_DENSITY_MARGIN")) margin = std::strtod(e, nullptr);
+#endif
+    if (nms && density > 0.0 && margin > 0.0) {
+        const double rows = (double)fdfk::kScoreListCap / (margin * density * (double)w) - 2.0;
         max_rows = rows < (double)g.nsub ? g.nsub : (rows > 256.0 ? 256u : (uint32_t)rows);
     }
     if (forced_rows) {   // fdf_ctx_set_band_rows: the height asked for, as far as LDS allows
@@ -247,10 +259,15 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         if (ctx->h_stats) {
             const uint64_t v = *reinterpret_cast<volatile uint64_t*>(ctx->h_stats);
             const uint32_t seq = (uint32_t)(v >> 32);
-            const fdf_ctx::LaunchInfo& li = ctx->hist[seq % 8];
-            if (seq != 0 && li.seq == seq && li.t == cfg->threshold && li.n == cfg->count &&
-                li.nms == cfg->nms && li.w == w && li.pixels > 0)
-                density = (double)(uint32_t)v / li.pixels;
+            const fdf_ctx::LaunchInfo& li = ctx->hist[seq % 64];
+            if (seq != 0 && li.seq == seq && li.pixels > 0) {
+                ctx->known[li.nms % 3] = li;
+                ctx->known_density[li.nms % 3] = (double)(uint32_t)v / li.pixels;
+            }
+            const fdf_ctx::LaunchInfo& k = ctx->known[cfg->nms % 3];
+            if (k.seq != 0 && k.t == cfg->threshold && k.n == cfg->count && k.nms == cfg->nms &&
+                k.w == w)
+                density = ctx->known_density[cfg->nms % 3];
         }
     }
     // workgroup slots of the device: 4 per CU (4 waves per SIMD); fdf_ctx_set_geometry's
@@ -260,6 +277,12 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows);
     const uint32_t R = geo.R;
     const uint32_t nw = (w + 31) / 32;
+#ifdef FDF_DEBUG_BUILD
+    if (std::getenv("FDF_GEOMETRY_LOG"))
+        std::fprintf(stderr, "fdf geometry: %u x %ux%u nms=%u t=%u n=%u density=%.5f R=%u nsub=%u\n",
+                     n_frames, w, h, (unsigned)cfg->nms, (unsigned)cfg->threshold,
+                     (unsigned)cfg->count, density, R, geo.nsub);
+#endif
     if (fdfk::make_sweep_layout(R, nw, cfg->nms).total > fdfk::kSweepMaxLds)
         return FDF_ERR_SIZE;
     const uint32_t bands = (h - 6 + R - 1) / R;
@@ -386,7 +409,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     c.stats_seq = 0;
     if (cfg->nms && ctx->h_stats && !direct) {
         const uint32_t seq = ++ctx->stats_seq == 0 ? ++ctx->stats_seq : ctx->stats_seq;
-        fdf_ctx::LaunchInfo& li = ctx->hist[seq % 8];
+        fdf_ctx::LaunchInfo& li = ctx->hist[seq % 64];
         li.seq = seq;
         li.t = cfg->threshold;
         li.n = cfg->count;

@@ -28,7 +28,11 @@ def main():
     ap.add_argument("--threshold", type=int, default=16)
     ap.add_argument("--count", type=int, default=9)
     ap.add_argument("--variants", default="maxt:0,maxt:2,maxt:3,off:0,off:2,off:3,sad:0")
+    ap.add_argument("--log-geometry", action="store_true",
+                    help="debug build: print each launch's band geometry to stderr")
     args = ap.parse_args()
+    if args.log_geometry:
+        os.environ["FDF_GEOMETRY_LOG"] = "1"
     import torch
 
     import workloads
@@ -38,8 +42,9 @@ def main():
     out = torch.empty((args.frames * 50_000, 2), dtype=torch.int32, device="cuda")
     offs = torch.zeros(args.frames + 1, dtype=torch.int64, device="cuda")
     modes = {"off": 0, "maxt": 1, "sad": 2}
-    # mode:flags[:lds_budget[:nsub[:rows]]] -- budget (bytes per workgroup), sub-bands per
-    # band and band rows (fdf_ctx_set_band_rows) override the geometry pick (0 = default)
+    # mode:flags[:lds_budget[:nsub[:rows[:margin]]]] -- budget (bytes per workgroup), sub-bands
+    # per band, band rows (fdf_ctx_set_band_rows) and the NMS density margin (debug build)
+    # override the geometry pick (0 = default)
     variants = [tuple(v.split(":")) for v in args.variants.split(",")]
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream()
@@ -48,7 +53,7 @@ def main():
         for v in variants:
             mode, flags = v[0], v[1]
             os.environ["FDF_DEBUG_FLAGS"] = str(int(flags, 0))
-            for k, name in ((2, "FDF_LDS_BUDGET"), (3, "FDF_NSUB")):
+            for k, name in ((2, "FDF_LDS_BUDGET"), (3, "FDF_NSUB"), (5, "FDF_DENSITY_MARGIN")):
                 if len(v) > k and v[k] != "0":
                     os.environ[name] = v[k]
                 else:
