@@ -172,7 +172,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     if (const char* e = std::getenv("FDF_NSUB")) g.nsub = std::max(1ul, std::strtoul(e, nullptr, 0));
 #endif
     const uint32_t centre_rows = h - 6;
-    const uint32_t nw = (w + 31) / 32;
+    const uint32_t nw = fdfk::bitmap_words_per_row(w);
     // extra rows a unit tests: NMS bands test one row above and below (first / last unit)
     const uint32_t halo = fdfk::band_halo(nms) * (g.nsub == 1 ? 2u : 1u);
     // LDS per workgroup sets the workgroups per CU: <= 40 KB keeps 4.
@@ -276,7 +276,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
                                           : (ctx->cus ? 4ull * ctx->cus : kDefaultMinTasks);
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows);
     const uint32_t R = geo.R;
-    const uint32_t nw = (w + 31) / 32;
+    const uint32_t nw = fdfk::bitmap_words_per_row(w);
 #ifdef FDF_DEBUG_BUILD
     if (std::getenv("FDF_GEOMETRY_LOG"))
         std::fprintf(stderr, "fdf geometry: %u x %ux%u nms=%u t=%u n=%u density=%.5f R=%u nsub=%u\n",

@@ -115,6 +115,13 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     return L;
 }
 
+// Words per bitmap row: ceil(W / 32) rounded up to a multiple of 4, so that every row of a
+// band's bitmap (LDS, and a slot holding it) starts 16-byte aligned and the emit reads 4
+// words of one row per lane (the pad words stay zero).
+__host__ __device__ inline uint32_t bitmap_words_per_row(uint32_t W) {
+    return ((W + 31) / 32 + 3) & ~3u;
+}
+
 // Sweep steps of a unit of `rows` owned rows plus `halo` extra tested rows, in whole
 // kSweepRing-step blocks (the 3 rows of vertical look-ahead are a prologue, not steps).
 __host__ __device__ inline uint32_t sweep_steps(uint32_t rows, uint32_t halo) {
@@ -165,7 +172,7 @@ struct BandParams {
     uint32_t rows;               // centre rows per band (R)
     uint32_t bands_per_frame;
     uint32_t ntasks;             // frames * bands_per_frame == grid size
-    uint32_t words_per_row;      // ceil(width / 32)
+    uint32_t words_per_row;      // bitmap_words_per_row(width)
     uint32_t threshold;
     uint32_t slot_bytes;
     uint8_t* slots;              // ntasks * slot_bytes

@@ -1240,13 +1240,19 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     if constexpr (kDebugBuild) ph[2] = __builtin_amdgcn_s_memtime();   // NMS done
 
     // ---- count keep-bits and write the band slot
-    // Each wave owns a contiguous quarter of the bitmap and sweeps it 64 words per round (lane
-    // = word): the word reads are independent and conflict-free, and a wave prefix sum of the
-    // words' keypoint counts places the round's points consecutively in the slot.
-    const uint32_t wq = (nwords + kWaves - 1) / kWaves;
-    const uint32_t wb = min(wave * wq, nwords), we = min(wb + wq, nwords);
+    // Each wave owns a contiguous quarter of the bitmap and sweeps it 256 words per round:
+    // lane = 4 words of one row (rows are whole 4-word groups, bitmap_words_per_row), one
+    // 16-byte LDS read each, and a wave prefix sum of the lanes' keypoint counts places the
+    // round's points consecutively in the slot.
+    const uint4* keep4 = reinterpret_cast<const uint4*>(keep);
+    const uint32_t ngroups = nwords / 4;
+    const uint32_t gq = (ngroups + kWaves - 1) / kWaves;
+    const uint32_t gb = min(wave * gq, ngroups), ge = min(gb + gq, ngroups);
     uint32_t mine = 0;
-    for (uint32_t w = wb + lane; w < we; w += 64) mine += __popc(keep[w]);
+    for (uint32_t g = gb + lane; g < ge; g += 64) {
+        const uint4 q = keep4[g];
+        mine += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+    }
     const uint32_t wave_total = __builtin_amdgcn_readlane(wave_incl_scan(mine), 63);
     if (lane == 0) wave_sum[wave] = wave_total;
     __syncthreads();
@@ -1272,18 +1278,25 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     if (listed || P.direct) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
         uint32_t o = before;
-        for (uint32_t w0 = wb; w0 < we; w0 += 64) {
-            const uint32_t w = w0 + lane;
-            uint32_t bits = w < we ? keep[w] : 0u;
-            const uint32_t c = __popc(bits);
+        for (uint32_t g0 = gb; g0 < ge; g0 += 64) {
+            const uint32_t g = g0 + lane;
+            const uint4 q = g < ge ? keep4[g] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t c = __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
             const uint32_t inc = wave_incl_scan(c);
             uint32_t idx = o + inc - c;
             o += __builtin_amdgcn_readlane(inc, 63);
-            const uint32_t r = udiv(w, nwd);
-            const uint32_t xb = (w - r * nw) * 32;
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
+            const uint32_t r = udiv(4 * g, nwd);
+            const uint32_t xb = (4 * g - r * nw) * 32;
+            uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+            while (lo | hi) {
+                uint32_t bit;
+                if (lo) {
+                    bit = (uint32_t)__builtin_ctzll(lo);
+                    lo &= lo - 1;
+                } else {
+                    bit = 64u + (uint32_t)__builtin_ctzll(hi);
+                    hi &= hi - 1;
+                }
                 const uint2 pt = make_uint2(xb + bit, y0 + r);
                 if (listed) pts[idx] = pt;
                 if (P.direct && dbase + idx < P.cap) P.out[dbase + idx] = pt;
