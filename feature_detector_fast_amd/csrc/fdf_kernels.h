@@ -92,6 +92,8 @@ static_assert(kScoreListCap % 256 == 0, "the spill NMS pass holds the list 1/256
 static_assert(kScoreListCap < 4096, "the LDS NMS pass keeps rank + 1 in a list entry's 12 score bits");
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
+    uint32_t seltab;             // during the sweep: the 256-entry set-bit table (1 KB) in
+                                 // the rank-prefix area, which NMS uses only after the sweep
     uint32_t nms_area_entries;   // u16 ranked scores that fit [pq, bprefix) after the sweep
 };
 
@@ -110,7 +112,9 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     L.bprefix = L.slist + cap * 4;
     L.nms_area_entries = (L.bprefix - L.pq) / 2;
     L.rprefix = L.bprefix + (nms ? align16(rows * nb * 2) : 0u);
-    L.misc = L.rprefix + (nms ? align16(rows * 4) : 0u);
+    L.seltab = L.bprefix;
+    const uint32_t prefix_end = L.rprefix + (nms ? align16(rows * 4) : 0u);
+    L.misc = prefix_end > L.seltab + 1024u ? prefix_end : L.seltab + 1024u;
     L.total = L.misc + 64;
     return L;
 }

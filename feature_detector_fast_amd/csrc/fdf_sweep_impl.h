@@ -155,15 +155,30 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
         return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b64(src.rs, o, 0, 0));
 }
 
+// FIFO entries keep a lane row's 16 candidate flags and its code (row - ys) << 6 | lane in
+// alternate nibbles: flag of lane column 4m + j at bit 8j + 4 + m, code nibble k at bits
+// 8k .. 8k+3 -- the sweep step builds the flags in that order from the compare bytes with
+// three bit-field inserts, and ORs in the code, instead of packing both into 16-bit halves.
+constexpr uint32_t kFlagNibbles = 0xF0F0F0F0u;
+__host__ __device__ constexpr uint32_t spread_code(uint32_t v) {   // 16 bits -> low nibbles
+    return (v & 0xFu) | ((v & 0xF0u) << 4) | ((v & 0xF00u) << 8) | ((v & 0xF000u) << 12);
+}
+// The low nibbles (or high nibbles, shifted down first) of x packed into 16 bits.
+__device__ __forceinline__ uint32_t pack_nibbles(uint32_t x) {
+    const uint32_t c = x | (x >> 4);                   // byte 0: nibbles 0, 1; byte 2: 2, 3
+    return __builtin_amdgcn_perm(c, c, 0x0c0c0200u);
+}
+
 struct SweepShared {
-    uint32_t* pq;          // kSweepPixelQ FIFO of lane rows with candidates: (row - ys) << 22 |
-                           // lane << 16 | 16-bit mask (bit b = lane column 4 (b & 3) + (b >> 2))
+    uint32_t* pq;          // kSweepPixelQ FIFO of lane rows with candidates (kFlagNibbles:
+                           // flags; low nibbles: spread_code((row - ys) << 6 | lane))
     uint32_t* stage;       // 64 pixels of the batch being issued: (row - ys) << 10 | strip column
     uint32_t* bitmap;      // band keypoints: bitmap row i = image row yb + i, words_per_row each
     uint32_t* slist;       // NMS: the band's keypoints as (bitmap row * W + x) << 12 | score
     uint32_t* slist_n;     // entries appended (the list, then the spill, then only counted)
     uint32_t slist_cap;    // kScoreListCap, or 0 when a position does not fit 20 bits
     uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
+    const uint32_t* seltab;  // select_bit's table (SweepLayout::seltab)
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
 };
 
@@ -260,17 +275,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 // Position of the j-th (from 0) set bit of a 16-bit mask that has more than j set bits.
-__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t j) {
-    uint32_t bit = 0;
-#pragma unroll
-    for (uint32_t w = 8; w >= 1; w >>= 1) {
-        const uint32_t c = __popc(m & ((1u << w) - 1u));
-        const bool up = j >= c;
-        j -= up ? c : 0u;
-        m = up ? m >> w : m;
-        bit += up ? w : 0u;
-    }
-    return bit;
+// seltab[b] holds the positions of byte b's set bits, the k-th in nibble k (built per
+// workgroup before its sweep), so the mask needs one byte choice and one LDS read instead
+// of four halving steps.
+__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t j, const uint32_t* seltab) {
+    const uint32_t c8 = (uint32_t)__popc(m & 0xffu);
+    const bool hi = j >= c8;
+    const uint32_t byte = hi ? m >> 8 : m & 0xffu;
+    const uint32_t jj = hi ? j - c8 : j;
+    return ((seltab[byte] >> (4u * jj)) & 7u) | (hi ? 8u : 0u);
 }
 
 // Pops the next 64 candidate pixels (fewer only when `force`: a flush) and starts their
@@ -308,45 +321,44 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
         const uint32_t lane = u.lane;
         const bool has = lane < nent;
         const uint32_t e = pk.e;
-        const uint32_t k = (uint32_t)__popc(e & 0xffffu);
+        uint32_t m = e & kFlagNibbles;
+        const uint32_t k = (uint32_t)__popc(m);
         const uint32_t inc = wave_incl_scan(k);
         const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
         if (total >= 64u || (force && total != 0u)) {
             b.n = min(total, 64u);
             const uint32_t excl = inc - k;
-            uint32_t m = e & 0xffffu;
             uint32_t scode = 0;
-            // no per-pixel loop: entry lane e marks the slot its pixels start at, a wave
-            // prefix-max turns the marks into each batch lane's entry, and the lane selects
-            // its bit of that entry's mask (binary search over popcounts)
+            // no per-pixel loop: entry lane e marks the slot its pixels start at, a ballot of
+            // the marks gives every batch lane its entry (the marks at or below it, less
+            // entry 0's, which always starts at slot 0), and the lane selects its bit of that
+            // entry's mask
             sh.stage[lane] = 0u;
-            if (has && k != 0u && excl < 64u) sh.stage[excl] = lane;
+            if (has && k != 0u && excl < 64u) sh.stage[excl] = 1u;
             // other lanes' stores feed this load: without the (instruction-free) wavefront
             // fence the compiler forwards the lane's own zero store (per-thread semantics)
             // and loads only where it stored
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            uint32_t src = sh.stage[lane];
-            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x111, 0xf, 0xf, false));
-            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x112, 0xf, 0xf, false));
-            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x114, 0xf, 0xf, false));
-            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x118, 0xf, 0xf, false));
-            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x142, 0xa, 0xf, false));
-            src = max(src, (uint32_t)__builtin_amdgcn_update_dpp(0u, src, 0x143, 0xc, 0xf, false));
+            const uint64_t starts = wave_ballot(sh.stage[lane] != 0u);
+            const uint32_t src = lanes_below(starts >> 1);
             const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)e);
             const uint32_t sx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)excl);
-            const uint32_t bit = select_bit(se & 0xffffu, lane - sx);
+            // the entry's flags as 16 bits: bit 4j + m = lane column 4m + j
+            const uint32_t bit = select_bit(pack_nibbles((se >> 4) & ~kFlagNibbles), lane - sx, sh.seltab);
             // stage code as the loop writes it: (row - ys) << 10 | lane << 4 | column,
             // kept in the lane (no LDS round trip: the lane reads only its own pixel)
-            scode = ((se >> 16) << 4) | ((bit & 3u) << 2) | (bit >> 2);
-            // the partial entry keeps the bits past the ones taken: batch lane 63 took its
+            scode = (pack_nibbles(se & ~kFlagNibbles) << 4) | ((bit & 3u) << 2) | (bit >> 2);
+            // the partial entry keeps the flags past the ones taken: batch lane 63 took its
             // last one (an entry is partial only when the batch is full), so one readlane
-            // replaces a second select
-            if (has && excl < 64u && inc > 64u)
-                m &= ~0u << (__builtin_amdgcn_readlane(bit, 63) + 1u);
+            // replaces a second select; flag 4j + m sits at entry bit 8j + 4 + m
+            if (has && excl < 64u && inc > 64u) {
+                const uint32_t b63 = __builtin_amdgcn_readlane(bit, 63);
+                m &= ~0u << (8u * (b63 >> 2) + 5u + (b63 & 3u));
+            }
             // entries [0, nfull) are taken whole; entry nfull keeps what is left of it
             const uint32_t nfull = (uint32_t)__popcll(wave_ballot(has && inc <= 64u));
             if (has && excl < 64u && inc > 64u)
-                sh.pq[(u.head + lane) & (kSweepPixelQ - 1)] = (e & 0xffff0000u) | m;
+                sh.pq[(u.head + lane) & (kSweepPixelQ - 1)] = (e & ~kFlagNibbles) | m;
             u.head += nfull;
             b.act = lane < b.n;
             if (b.act) {
@@ -566,16 +578,17 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     const int W = (int)u.src.W;
     const int xb = u.S - LC + LC * (int)lane;
     // candidate columns of this lane: the strip's centres (halo lanes 0 and 63 own none)
-    // (bit 8j + m = lane column 4m + j, the order the candidate mask is built in)
+    // (bit 8j + 4 + m = lane column 4m + j, the order the FIFO entry's flags are built in)
     uint32_t vmask = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int x = xb + 4 * m + j;
-            if (x >= 3 && x < W - 3 && lane >= 1 && lane <= 62) vmask |= 1u << (8 * j + m);
+            if (x >= 3 && x < W - 3 && lane >= 1 && lane <= 62) vmask |= 1u << (8 * j + 4 + m);
         }
     }
+    const uint32_t lane_code = spread_code(lane);
     const int p0 = u.p0, p1 = u.p1;                    // rows run through the pre-filter
     const int ys = p0;                                 // first swept row
     u.ys = ys;
@@ -647,18 +660,20 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
             }                                                                                \
         }                                                                                    \
         /* the lane row's candidates into the FIFO as one entry: column 4m + j of the */     \
-        /* lane is bit 8j + m of cm, then bit 4j + m of the 16-bit mask */                   \
-        uint32_t cm = 0;                                                                     \
-        _Pragma("unroll") for (int m = 0; m < M; ++m) cm |= (cand[m] >> (7 - m)) & (0x01010101u << m); \
-        cm &= live ? vmask : 0u;                                                             \
-        {                                                                                    \
-            const uint32_t cx = cm | (cm >> 4);                                              \
-            const uint32_t m16 = __builtin_amdgcn_perm(cx, cx, 0x0c0c0200u);                 \
-            const bool has = m16 != 0u;                                                      \
+        /* lane is bit 8j + 4 + m (bit 7 of byte j of cand[m], moved by bit-field */         \
+        /* inserts), the row and lane code in the low nibbles */                             \
+        static_assert(M == 4, "four flag dwords per lane row");                              \
+        uint32_t cm = cand[3];                           \
+        cm = (cm & 0x80808080u) | ((cand[2] >> 1) & ~0x80808080u);                           \
+        cm = (cm & 0xC0C0C0C0u) | ((cand[1] >> 2) & ~0xC0C0C0C0u);                           \
+        cm = (cm & 0xE0E0E0E0u) | ((cand[0] >> 3) & ~0xE0E0E0E0u);                           \
+        cm &= vmask;                                                                         \
+        if (live) {                                                                          \
+            const bool has = cm != 0u;                                                       \
             const uint64_t bal = wave_ballot(has);                                           \
             if (has)                                                                         \
                 sh.pq[(u.tail + lanes_below(bal)) & (kSweepPixelQ - 1)] =                    \
-                    ((uint32_t)(i0 + (J)) << 22) | (lane << 16) | m16;                       \
+                    cm | lane_code | row_code | spread_code((uint32_t)(J) << 6);             \
             u.tail += (uint32_t)__popcll(bal);                                               \
             while (u.tail - u.head > kSweepPixelQ - 64) {                                    \
                 /* dense image: test the oldest pixels now, synchronously */                 \
@@ -679,10 +694,12 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         }                                                                                    \
     }
 
-    static_assert(K == 8 || K == 12 || K == 16, "ring of 8, 12 or 16 rows");
+    static_assert(K == 8 || K == 16, "ring of 8 or 16 rows (a power of two: row codes OR together)");
     static_assert((K / kIssue) % kSweepBatchSlots == 0 || kSweepBatchSlots == 1,
                   "issue points per loop body must cycle through the batch slots");
     for (int i0 = 0; i0 < T; i0 += K) {
+        // FIFO code of row ys + i0 + J: i0 is a multiple of K, so its spread ORs with J's
+        const uint32_t row_code = spread_code((uint32_t)i0 << 6);
         FDF_SWEEP_STEP(0)
         FDF_SWEEP_STEP(1)
         FDF_SWEEP_STEP(2)
@@ -1134,6 +1151,17 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         unit_ctr[0] = 0;
         unit_ctr[1] = 0;
     }
+    {   // select_bit's table: the positions of byte tid's set bits, the k-th in nibble k
+        static_assert(kThreads == 256, "one table entry per thread");
+        uint32_t word = 0, k = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t bit = (tid >> i) & 1u;
+            word |= bit ? i << (4u * k) : 0u;
+            k += bit;
+        }
+        reinterpret_cast<uint32_t*>(smem_raw + L.seltab)[tid] = word;
+    }
     __syncthreads();
     if constexpr (kDebugBuild) ph[0] = __builtin_amdgcn_s_memtime();   // setup done
 
@@ -1147,6 +1175,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     sh.slist_cap = (uint64_t)(rows + 2 * halo) * W <= (1u << 20) ? kScoreListCap : 0u;
     sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
     sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
+    sh.seltab = reinterpret_cast<const uint32_t*>(smem_raw + L.seltab);
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;

@@ -10,6 +10,7 @@
 #                                      tools/ablate.py variants)       -> NAME.txt
 #   ablate|NAME|ARGS                   tools/ablate.py ARGS on the debug build -> NAME.json
 #   pmc|NAME|VARIANT|ARGS              SQ / TCC counter passes of one variant (debug build)
+#   pmcv|NAME|VARIANTS|ARGS            one instruction-count pass per variant (debug build)
 #   stamps|NAME|ARGS                   tools/stamps.py ARGS (debug build) -> NAME.json
 #   profile|TAG|ARGS                   tools/profile_round.sh TAG ARGS (kernel stats + traffic)
 #   single|NAME                        single-frame latency + kernel traces (off, max-t)
@@ -59,6 +60,18 @@ for STEP in "$@"; do
             python3 tools/ablate.py --rounds 1 --iters 2 $A3 --variants "$A2" > "$D/p$j.log" 2>&1 || fail "$STEP pass $j" "$D/p$j.log"
       done
       python3 tools/pmc_summary.py "$D"/p* > "$O/$A1.txt" 2>&1 || fail "$STEP summary" "$O/$A1.txt"
+      cat "$O/$A1.txt"
+      rm -rf "$D" ;;
+    pmcv)
+      # one instruction-count pass per variant (comma-separated): where the issue cycles go
+      D="$O/$A1"; mkdir -p "$D"; : > "$O/$A1.txt"
+      IFS=',' read -r -a VS <<< "$A2"
+      for v in "${VS[@]}"; do
+        t=$(echo "$v" | tr ':.' '__')
+        FDF_LIB_PATH=$DEBUG_LIB timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d "$D/$t" -o p --output-format csv -- \
+            python3 tools/ablate.py --rounds 1 --iters 2 $A3 --variants "$v" > "$D/$t.log" 2>&1 || fail "$STEP $v" "$D/$t.log"
+        echo "$v $(python3 tools/pmc_summary.py "$D/$t" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(json.dumps({k: round(v) for k, v in d.items() if not k.startswith("_")}))')" >> "$O/$A1.txt"
+      done
       cat "$O/$A1.txt"
       rm -rf "$D" ;;
     stamps)
