@@ -201,9 +201,10 @@ class Context:
     def stream(self):
         return self._lib.fdf_ctx_stream(self.handle)
 
-    def set_timing(self, enable=True):
-        """Record HIP events around the detector and compaction launches of each call."""
-        check(self._lib.fdf_ctx_set_timing(self.handle, 1 if enable else 0))
+    def set_timing(self, enable=True, every=1):
+        """Record the detector and compaction kernel durations of every `every`-th call
+        (dispatch-timestamped HIP events; fdf_ctx_set_timing)."""
+        check(self._lib.fdf_ctx_set_timing(self.handle, max(1, int(every)) if enable else 0))
 
     def timing(self):
         """(calls, detector_ms_total, compaction_ms_total) since timing was enabled."""

@@ -76,10 +76,13 @@ struct fdf_ctx {
     // grid size that counts as filling the chip (fdf_ctx_set_geometry; 0 = kDefaultMinTasks)
     uint64_t min_tasks = 0;
     uint32_t band_rows = 0;              // fdf_ctx_set_band_rows (0 = automatic)
-    // optional per-kernel timing (fdf_ctx_set_timing): 3 events around each call's launches
-    bool timing = false;
+    // optional per-kernel timing (fdf_ctx_set_timing): every `timing`-th call (0: off) records
+    // its kernels' durations
+    uint32_t timing = 0;
+    uint64_t timing_calls = 0;            // calls since timing was enabled
     size_t timed = 0;                     // calls recorded since timing was enabled
-    std::vector<hipEvent_t> ev;           // 3 per recorded call, kMaxTimedCalls at most
+    std::vector<hipEvent_t> ev;           // 4 per recorded call, kMaxTimedCalls at most
+    std::vector<uint8_t> timed_compact;   // per recorded call: 1 if it launched the compaction
     // direct output of small grids (BandParams::direct): look-back descriptors, launch tag
     uint64_t* d_lookback = nullptr;       size_t lookback_n = 0;
     uint32_t cus = 0;                     // compute units of the device
@@ -421,29 +424,33 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         c.stats_out = ctx->d_stats;
         c.stats_seq = seq;
     }
+    // per-kernel timing: 4 events per call, timestamped by the dispatches themselves
+    // (hipExtLaunchKernelGGL), so no marker packets sit between the kernels
     hipEvent_t* ev = nullptr;
-    if (ctx->timing && ctx->timed < kMaxTimedCalls) {
-        while (ctx->ev.size() < 3 * (ctx->timed + 1)) {
+    if (ctx->timing && ctx->timing_calls++ % ctx->timing == 0 && ctx->timed < kMaxTimedCalls) {
+        while (ctx->ev.size() < 4 * (ctx->timed + 1)) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return FDF_ERR_DEVICE;
             ctx->ev.push_back(e);
         }
-        ev = &ctx->ev[3 * ctx->timed];
+        ev = &ctx->ev[4 * ctx->timed];
     }
-    if (ev && hipEventRecord(ev[0], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    if ((rgb ? fdfk::launch_sweep_rgb(p, cfg->nms, cfg->count, stream)
-             : fdfk::launch_sweep(p, cfg->nms, cfg->count, stream)) != hipSuccess) {
+    if ((rgb ? fdfk::launch_sweep_rgb(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr,
+                                      ev ? ev[1] : nullptr)
+             : fdfk::launch_sweep(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr,
+                                  ev ? ev[1] : nullptr)) != hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
-    if (ev && hipEventRecord(ev[1], stream) != hipSuccess) return FDF_ERR_DEVICE;
-    if (!direct && fdfk::launch_compact(c, stream) != hipSuccess) {
+    if (!direct && fdfk::launch_compact(c, stream, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr) !=
+                       hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
     if (grouped) ctx->sums_parity ^= 1;
     if (ev) {
-        if (hipEventRecord(ev[2], stream) != hipSuccess) return FDF_ERR_DEVICE;
+        if (ctx->timed_compact.size() <= ctx->timed) ctx->timed_compact.resize(ctx->timed + 1);
+        ctx->timed_compact[ctx->timed] = direct ? 0 : 1;
         ++ctx->timed;
     }
     ctx->last_compact = c;
@@ -724,8 +731,9 @@ void* fdf_ctx_stream(fdf_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->s
 int fdf_ctx_set_timing(fdf_ctx* ctx, int enable) {
     if (!ctx) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);
-    ctx->timing = enable != 0;
+    ctx->timing = enable > 0 ? (uint32_t)enable : 0u;
     ctx->timed = 0;
+    ctx->timing_calls = 0;
     return FDF_OK;
 }
 
@@ -753,19 +761,28 @@ int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows) {
     return FDF_OK;
 }
 
+// Kernel durations of recorded call k (0 for a compaction the call did not launch).
+static int timed_call(fdf_ctx* ctx, size_t k, float* detect_ms, float* compact_ms) {
+    const hipEvent_t* e = &ctx->ev[4 * k];
+    const bool compact = k < ctx->timed_compact.size() && ctx->timed_compact[k];
+    *compact_ms = 0.0f;
+    if (hipEventSynchronize(e[1]) != hipSuccess ||
+        hipEventElapsedTime(detect_ms, e[0], e[1]) != hipSuccess)
+        return FDF_ERR_DEVICE;
+    if (compact && (hipEventSynchronize(e[3]) != hipSuccess ||
+                    hipEventElapsedTime(compact_ms, e[2], e[3]) != hipSuccess))
+        return FDF_ERR_DEVICE;
+    return FDF_OK;
+}
+
 int fdf_ctx_timing_samples(fdf_ctx* ctx, float* detect_ms, float* compact_ms, uint32_t cap,
                            uint32_t* n) {
     if (!ctx || !n || (cap && (!detect_ms || !compact_ms))) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);
     DeviceGuard guard(ctx->device);
     *n = (uint32_t)ctx->timed;
-    for (size_t k = 0; k < ctx->timed && k < cap; ++k) {
-        const hipEvent_t* e = &ctx->ev[3 * k];
-        if (hipEventSynchronize(e[2]) != hipSuccess ||
-            hipEventElapsedTime(&detect_ms[k], e[0], e[1]) != hipSuccess ||
-            hipEventElapsedTime(&compact_ms[k], e[1], e[2]) != hipSuccess)
-            return FDF_ERR_DEVICE;
-    }
+    for (size_t k = 0; k < ctx->timed && k < cap; ++k)
+        if (timed_call(ctx, k, &detect_ms[k], &compact_ms[k]) != FDF_OK) return FDF_ERR_DEVICE;
     return FDF_OK;
 }
 
@@ -776,12 +793,8 @@ int fdf_ctx_timing(fdf_ctx* ctx, uint32_t* calls, float* detect_ms, float* compa
     *calls = (uint32_t)ctx->timed;
     *detect_ms = *compact_ms = 0.0f;
     for (size_t k = 0; k < ctx->timed; ++k) {
-        const hipEvent_t* e = &ctx->ev[3 * k];
         float a = 0.0f, b = 0.0f;
-        if (hipEventSynchronize(e[2]) != hipSuccess ||
-            hipEventElapsedTime(&a, e[0], e[1]) != hipSuccess ||
-            hipEventElapsedTime(&b, e[1], e[2]) != hipSuccess)
-            return FDF_ERR_DEVICE;
+        if (timed_call(ctx, k, &a, &b) != FDF_OK) return FDF_ERR_DEVICE;
         *detect_ms += a;
         *compact_ms += b;
     }

@@ -36,9 +36,9 @@ constexpr bool kDebugBuild = false;
 // Debug builds: per-workgroup stamps of the detector (BandParams::stamps, kStampWords words per
 // workgroup): shader clock and 100 MHz real time at the workgroup's start and end, its XCD
 // and hardware id, its band, and the shader clock at the end of its phases as wave 0 sees
-// them (setup, its sweep, NMS, look-back).  Written only to that buffer; no output depends
-// on them.
-constexpr uint32_t kStampWords = 10;
+// them (setup, its sweep, NMS, look-back), and the low 32 bits of the shader clock at each
+// wave's sweep end.  Written only to that buffer; no output depends on them.
+constexpr uint32_t kStampWords = 12;
 
 // Column-sweep kernel (fdf_sweep.hip).  Lane l of a wave owns kLaneCols columns; a strip is
 // 62 lanes wide (lanes 0 and 63 are halo lanes).
@@ -206,10 +206,15 @@ constexpr uint64_t kLbValue = kLbAggregate - 1;
 // the CU count times the workgroups one CU holds (host side, fdf_api.cpp).
 constexpr uint32_t kDirectMaxTasks = 1024;
 
-hipError_t launch_compact(const CompactParams& c, hipStream_t stream);
-hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
+// start / stop (optional): events the dispatch itself timestamps (hipExtLaunchKernelGGL), so
+// per-kernel timing adds no packets between the kernels
+hipError_t launch_compact(const CompactParams& c, hipStream_t stream, hipEvent_t start = nullptr,
+                          hipEvent_t stop = nullptr);
+hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
+                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // RGB8 frames (3 bytes per pixel, frame_stride in bytes), luma converted on load
-hipError_t launch_sweep_rgb(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream);
+hipError_t launch_sweep_rgb(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
+                            hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_rgb_to_luma(const uint8_t* rgb, uint32_t n_frames, uint32_t pixels,
                               uint64_t rgb_frame_stride, uint8_t* grey, hipStream_t stream);
 hipError_t launch_score_rings(const uint8_t* centers, const uint8_t* rings, uint32_t nrings,

@@ -10,6 +10,7 @@
 //   own score functions (fdf_score_rings; src/fast_simd.rs:623, :722).
 // rgb_to_luma_kernel -- RGB8 -> grey exactly as image 0.24.6's to_luma8, which the
 //   reference's callers apply before detect (src/main.rs:58, tests/compare.rs:33).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -158,11 +159,16 @@ hipError_t launch_score_rings(const uint8_t* centers, const uint8_t* rings, uint
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const CompactParams& c, hipStream_t stream) {
+hipError_t launch_compact(const CompactParams& c, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop) {
     if (c.tasks_per_group == 0 || c.tasks_per_group > (uint32_t)kCompactTasks)
         return hipErrorInvalidValue;
     const uint32_t ngroups = (c.ntasks + c.tasks_per_group - 1) / c.tasks_per_group;
-    hipLaunchKernelGGL(compact_kernel, dim3(ngroups), dim3(kCompactTasks), 0, stream, c);
+    if (start || stop)
+        hipExtLaunchKernelGGL(compact_kernel, dim3(ngroups), dim3(kCompactTasks), 0, stream, start,
+                              stop, 0, c);
+    else
+        hipLaunchKernelGGL(compact_kernel, dim3(ngroups), dim3(kCompactTasks), 0, stream, c);
     return hipGetLastError();
 }
 

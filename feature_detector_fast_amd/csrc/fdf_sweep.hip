@@ -4,7 +4,8 @@
 #include "fdf_sweep_impl.h"
 
 namespace fdfk {
-hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream) {
-    return grey::launch(p, nms, n, stream);
+hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
+                        hipEvent_t start, hipEvent_t stop) {
+    return grey::launch(p, nms, n, stream, start, stop);
 }
 }  // namespace fdfk

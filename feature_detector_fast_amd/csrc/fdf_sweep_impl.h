@@ -32,6 +32,7 @@
 // keypoint is compared with the scores of the neighbours the bitmap marks.  The band's
 // keep-bits are then written to its output slot (its points in raster order, or the bitmap
 // if they do not fit) and compact_kernel orders all slots.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -729,25 +730,25 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
 // words are read unconditionally (the bitmap has a pad word after its last row).
 __device__ __forceinline__ uint32_t bits3(const uint32_t* row, int x) {
     const int xm = x - 1, wi = xm >> 5, sh = xm & 31;
-    const uint64_t v = ((uint64_t)row[wi + 1] << 32) | row[wi];
-    return (uint32_t)(v >> sh) & 7u;
+    return __builtin_amdgcn_alignbit(row[wi + 1], row[wi], (uint32_t)sh) & 7u;   // funnel shift
 }
 
 // Raster rank of bitmap position (row, x): keypoints before it in the band's bitmap.
-// rprefix[row] counts the rows above, bprefix[row * nb + k] the words [0, 4k) of the row.
+// bprefix[row * nb + k] counts the keypoints before word 4k of the row (all rows above
+// included); the position's 4-word block is one 16-byte LDS read (bitmap rows are whole
+// blocks, bitmap_words_per_row).
 __device__ __forceinline__ uint32_t bitmap_rank(const uint32_t* bitmap, const uint16_t* bprefix,
-                                                const uint32_t* rprefix, uint32_t nw, uint32_t nb,
-                                                uint32_t row, uint32_t x) {
-    static_assert(kRankBlock == 4, "three block words before the position's word");
-    const uint32_t wi = x >> 5, blk = wi / kRankBlock, w0 = blk * kRankBlock;
-    const uint32_t* rw = bitmap + row * nw;
-    uint32_t r = rprefix[row] + bprefix[row * nb + blk];
-#pragma unroll
-    for (uint32_t j = 0; j < kRankBlock - 1; ++j) {
-        const uint32_t v = rw[min(w0 + j, wi)];         // in-row, read unconditionally
-        r += w0 + j < wi ? __popc(v) : 0u;
-    }
-    return r + __popc(rw[wi] & ((1u << (x & 31)) - 1u));
+                                                const uint32_t* /*rprefix*/, uint32_t nw,
+                                                uint32_t nb, uint32_t row, uint32_t x) {
+    static_assert(kRankBlock == 4, "one 16-byte block per rank prefix");
+    const uint32_t wi = x >> 5, blk = wi / kRankBlock, j = wi % kRankBlock;
+    const uint4 q = reinterpret_cast<const uint4*>(bitmap + row * nw)[blk];
+    uint32_t r = bprefix[row * nb + blk];
+    r += j > 0 ? (uint32_t)__popc(q.x) : 0u;
+    r += j > 1 ? (uint32_t)__popc(q.y) : 0u;
+    r += j > 2 ? (uint32_t)__popc(q.z) : 0u;
+    const uint32_t w = j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
+    return r + (uint32_t)__popc(w & ((1u << (x & 31)) - 1u));
 }
 
 // Neighbour bits of bitmap position (row, x) among the R2 bitmap rows: bit k of the up /
@@ -760,9 +761,9 @@ __device__ __forceinline__ uint32_t neighbour_bits(const uint32_t* bitmap, uint3
            (row + 1 < R2 ? bits3(bitmap + (row + 1) * nw, (int)x) : 0u);
 }
 
-// Rank prefixes of the band's keypoint bitmap (R2 rows): rprefix[row] = keypoints in the
-// rows above, bprefix[row * nb + k] = keypoints in words [0, 4k) of the row.  Returns the
-// bitmap's keypoint total (every thread).
+// Rank prefixes of the band's keypoint bitmap (R2 rows): bprefix[row * nb + k] = keypoints
+// before word 4k of the row, the rows above included (rprefix: the row prefixes on the
+// way).  Returns the bitmap's keypoint total (every thread).
 __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint32_t nw,
                                        uint16_t* bprefix, uint32_t* rprefix, uint32_t* total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -830,6 +831,14 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
         if (lane == 0) *total = carry;
     }
     __syncthreads();
+    // block prefixes absolute (the rows above included): one read per rank (u16 holds them:
+    // the ranked tiers hold at most nms_area_entries keypoints)
+    {
+        const RowDiv nbd = make_rowdiv(nb_blocks);
+        for (uint32_t i = tid; i < R2 * nb_blocks; i += kThreads)
+            bprefix[i] = (uint16_t)(bprefix[i] + rprefix[udiv(i, nbd)]);
+    }
+    __syncthreads();
     return *total;
 }
 
@@ -843,9 +852,10 @@ __device__ uint32_t band_rank_prefixes(const uint32_t* bitmap, uint32_t R2, uint
 template <bool RANKED>
 __device__ __forceinline__ uint32_t nms_entry(uint32_t e, const uint32_t* bitmap, uint32_t nw,
                                               uint32_t nb_blocks, uint32_t y0, RowDiv W,
-                                              uint32_t H, const uint16_t* sranked,
+                                              uint32_t H, uint32_t R2, const uint16_t* sranked,
                                               const uint16_t* bprefix, const uint32_t* rprefix) {
     const uint32_t pos = e >> 12, row = udiv(pos, W), x = pos - row * W;
+    if (row == 0 || row == R2 - 1) return e;          // bitmap rows 0, R2-1: neighbours only
     const uint32_t y = y0 - 1 + row;
     const uint32_t low = e & 0xfffu;
     bool suppressed = y == 3 || y == H - 4;
@@ -900,11 +910,6 @@ __device__ __forceinline__ void nms_clear(uint32_t e, uint32_t* bitmap, uint32_t
     }
 }
 
-__device__ __forceinline__ bool in_band_rows(uint32_t e, RowDiv W, uint32_t R2) {
-    const uint32_t row = udiv(e >> 12, W);
-    return row != 0 && row != R2 - 1;                 // bitmap rows 0, R2-1: neighbours only
-}
-
 // Band NMS (src/fast_simd.rs:589-616) from the band's score list, in place on the keypoint
 // bitmap (bitmap rows 0 and rows + 1 are the rows just outside the band, neighbours only).
 // The list holds every keypoint of the bitmap once; its scores are scattered into raster
@@ -927,11 +932,9 @@ __device__ void band_nms_lds(uint32_t* bitmap, uint32_t rows, uint32_t nw, uint3
         slist[i] = nms_scatter<true>(slist[i], bitmap, nw, R2, nb_blocks, W, sranked, bprefix,
                                      rprefix);
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kThreads) {
-        const uint32_t e = slist[i];
-        if (in_band_rows(e, W, R2))
-            slist[i] = nms_entry<true>(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
-    }
+    for (uint32_t i = tid; i < n; i += kThreads)
+        slist[i] = nms_entry<true>(slist[i], bitmap, nw, nb_blocks, y0, W, H, R2, sranked, bprefix,
+                                   rprefix);
     __syncthreads();
     for (uint32_t i = tid; i < n; i += kThreads) nms_clear(slist[i], bitmap, nw, W);
     __syncthreads();
@@ -958,13 +961,11 @@ __device__ void band_nms_spill(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j)
-        if (in_band_rows(ent[j], W, R2))
-            ent[j] = nms_entry<false>(ent[j], bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
-    for (uint32_t i = tid; i < n - cap; i += kThreads) {
-        const uint32_t e = spill[i];
-        if (in_band_rows(e, W, R2))
-            spill[i] = nms_entry<false>(e, bitmap, nw, nb_blocks, y0, W, H, sranked, bprefix, rprefix);
-    }
+        ent[j] = nms_entry<false>(ent[j], bitmap, nw, nb_blocks, y0, W, H, R2, sranked, bprefix,
+                                  rprefix);
+    for (uint32_t i = tid; i < n - cap; i += kThreads)
+        spill[i] = nms_entry<false>(spill[i], bitmap, nw, nb_blocks, y0, W, H, R2, sranked, bprefix,
+                                    rprefix);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kSpillPer; ++j) nms_clear(ent[j], bitmap, nw, W);
@@ -1231,7 +1232,12 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         if constexpr (NMS == kNmsMaxThreshold)
             if (u.kq_n != 0) score_kp_queue<N>(sh, u, u.kq_n);
     }
-    if constexpr (kDebugBuild) ph[1] = __builtin_amdgcn_s_memtime();   // this wave's sweep done
+    if constexpr (kDebugBuild) {
+        ph[1] = __builtin_amdgcn_s_memtime();   // this wave's sweep done
+        // every wave's sweep end (low 32 bits of the shader clock), for the stamps
+        if (P.stamps && lane == 0)
+            reinterpret_cast<uint32_t*>(smem_raw + L.misc + 48)[wave] = (uint32_t)ph[1];
+    }
     __syncthreads();
 
     const uint32_t nwords = rows * nw;
@@ -1377,6 +1383,10 @@ void fast_sweep_kernel(BandParams P) {
                        (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
                 s[5] = task;
                 for (int k = 0; k < 4; ++k) s[6 + k] = ph[k];   // phases (wave 0's view)
+                const uint32_t* we = reinterpret_cast<const uint32_t*>(smem_raw +
+                    make_sweep_layout(P.rows, P.words_per_row, NMS).misc + 48);
+                s[10] = ((uint64_t)we[1] << 32) | we[0];          // waves' sweep ends
+                s[11] = ((uint64_t)we[3] << 32) | we[2];
             }
         }
     }
@@ -1399,7 +1409,8 @@ static SweepKernelFn pick_sweep_n(uint32_t n) {
     }
 }
 
-hipError_t launch(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream) {
+hipError_t launch(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
+                  hipEvent_t start, hipEvent_t stop) {
     SweepKernelFn fn = nullptr;
     switch (nms) {
         case kNmsOff: fn = pick_sweep_n<kNmsOff>(n); break;
@@ -1416,7 +1427,10 @@ hipError_t launch(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t str
                                            (int)L.total);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
+    if (start || stop)
+        hipExtLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, start, stop, 0, p);
+    else
+        hipLaunchKernelGGL(fn, dim3(p.ntasks), dim3(kThreads), L.total, stream, p);
     return hipGetLastError();
 }
 

@@ -87,10 +87,14 @@ void fdf_ctx_destroy(fdf_ctx* ctx);
 void* fdf_ctx_stream(fdf_ctx* ctx);
 
 /* Profiling (extension, no reference counterpart): while enabled, each detect call on the
- * context (up to 4096 of them) records HIP events on its stream around its two kernel
- * launches -- the detector (pre-filter, segment test, NMS, per-band slots) and the
- * raster-order compaction.  fdf_ctx_timing waits for the recorded calls and returns their
- * number and the summed durations of both launches in ms.  Enabling resets the record. */
+ * context (up to 4096 of them) records the durations of its two kernel launches -- the
+ * detector (pre-filter, segment test, NMS, per-band slots) and the raster-order compaction
+ * -- with HIP events the dispatches themselves timestamp (no packets between the kernels).
+ * A call whose grid writes its points directly has no compaction launch: 0 ms.
+ * enable = k > 1 records every k-th call only (the timestamped dispatches cost ~10 us each
+ * on the queue, so a timed run samples).  fdf_ctx_timing waits for the recorded calls and
+ * returns their number and the summed durations of both launches in ms.  Enabling resets the
+ * record. */
 int fdf_ctx_set_timing(fdf_ctx* ctx, int enable);
 int fdf_ctx_timing(fdf_ctx* ctx, uint32_t* calls, float* detect_ms, float* compact_ms);
 /* The same record per call: *n = calls recorded; the first `cap` calls' detector and

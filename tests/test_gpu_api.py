@@ -126,20 +126,25 @@ def test_geometry_override_same_result():
 
 
 def test_timing_samples():
+    """Per-call kernel durations from the dispatch-stamped events: an 8-frame batch writes
+    its points directly (no compaction launch: 0 ms), a 64-frame batch runs both kernels."""
     import torch
 
-    frames = workloads.s1_frames_torch(0, 8)
-    out = torch.empty((8 * 20000, 2), dtype=torch.int32, device="cuda")
-    offs = torch.zeros(9, dtype=torch.int64, device="cuda")
     ctx = fast_hip.context(0)
-    ctx.set_timing(True)
-    for _ in range(5):
-        fast_hip.detect_device(frames, Config(16, 9, NonMaximalSuppression.Off), out, offs)
-    det, com = ctx.timing_samples()
-    calls, d_tot, c_tot = ctx.timing()
-    ctx.set_timing(False)
-    assert calls == 5 and det.shape == (5,) and np.all(det > 0) and np.all(com > 0)
-    assert abs(float(det.sum()) - d_tot) < 1e-3 * max(d_tot, 1.0)
+    for F, direct in ((8, True), (64, False)):
+        frames = workloads.s1_frames_torch(0, F)
+        out = torch.empty((F * 20000, 2), dtype=torch.int32, device="cuda")
+        offs = torch.zeros(F + 1, dtype=torch.int64, device="cuda")
+        ctx.set_timing(True)
+        for _ in range(5):
+            fast_hip.detect_device(frames, Config(16, 9, NonMaximalSuppression.Off), out, offs)
+        det, com = ctx.timing_samples()
+        calls, d_tot, c_tot = ctx.timing()
+        ctx.set_timing(False)
+        assert calls == 5 and det.shape == (5,) and np.all(det > 0)
+        assert np.all(com == 0) if direct else np.all(com > 0)
+        assert abs(float(det.sum()) - d_tot) < 1e-3 * max(d_tot, 1.0)
+        assert abs(float(com.sum()) - c_tot) < 1e-3 * max(c_tot, 1.0)
 
 
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("FDF_LIB_PATH", os.path.join(ROOT, "build", "libfdf_debug.so"))
 os.environ["FDF_STAMPS"] = "1"
-WORDS = 10
+WORDS = 12
 
 
 def summarize(st, ntasks_expected):
@@ -63,7 +63,15 @@ def summarize(st, ntasks_expected):
             prev = np.where(ok, m, prev)
     phases["emit_end"] = round(float(np.median(marks[:, -1] - prev)), 0)
     phases["total_cycles"] = round(float(np.median(t1 - t0)), 0)
-    return {"phases_cycles_p50": phases,
+    # the four waves' sweep ends (low 32 bits of the shader clock) relative to the start
+    ends = np.stack([st[:, 10] & 0xFFFFFFFF, st[:, 10] >> 32, st[:, 11] & 0xFFFFFFFF,
+                     st[:, 11] >> 32], axis=1)
+    rel = (ends - (t0[:, None] & 0xFFFFFFFF)) % (1 << 32)
+    spread = rel.max(axis=1) - rel.min(axis=1)
+    waves = {"sweep_end_spread_cycles_p50_p90": [round(float(np.percentile(spread, q)), 0) for q in (50, 90)],
+             "spread_over_slowest_sweep_p50": round(float(np.median(spread / np.maximum(rel.max(axis=1), 1))), 3),
+             "slowest_wave_share": [round(float(np.mean(rel.argmax(axis=1) == w)), 3) for w in range(4)]}
+    return {"phases_cycles_p50": phases, "waves": waves,
         "workgroups": int(len(st)), "ntasks": int(ntasks_expected),
         "span_us": round(span, 2),
         "cus_seen": len(first_per_cu),
