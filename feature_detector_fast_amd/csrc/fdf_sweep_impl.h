@@ -1098,6 +1098,14 @@ __device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t t
     // tail.
 __device__ __forceinline__ uint32_t band_task(const BandParams& P) {
     const uint32_t b = blockIdx.x;
+#ifdef FDF_LINEAR_TASKS
+    {   // A/B variant: block b -> the b-th band in raster order over the whole grid (the
+        // frames' full bands first, their last bands at the end), no XCD ranges
+        const uint32_t B = P.bands_per_frame, nfull = (P.ntasks / B) * (B - 1);
+        if (B <= 1) return b;
+        return b < nfull ? (b / (B - 1)) * B + b % (B - 1) : (b - nfull) * B + (B - 1);
+    }
+#endif
     const uint32_t q8 = P.ntasks >> 3, r8 = P.ntasks & 7, k8 = b & 7;
     const uint32_t c0 = k8 * q8 + min(k8, r8), j = b >> 3;
     uint32_t task = c0 + j;

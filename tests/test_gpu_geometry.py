@@ -157,3 +157,46 @@ def test_direct_output_4k_frame_and_capacity():
     assert int(offs[1]) == len(want) and int(offs[0]) == 0
     assert np.array_equal(out.cpu().numpy().astype(np.uint32), want[:cap])
     assert np.array_equal(fast_hip.detect_array(img, Config(8, 12, NonMaximalSuppression.Off)), want)
+
+
+@pytest.mark.parametrize("nms", [0, 1, 2])
+def test_many_band_batches(nms):
+    """A grid of more bands than the device holds workgroups at once (8-row bands: ~1 400
+    bands, run in rounds), 24 frames of 640x480 mixing S1, S2 and dense S3, launched 4 times
+    on one context: every launch equals the first and every frame equals the oracle.  (The
+    persistent-grid experiment of round 3, branch exp-persistent-grid, ran this test.)"""
+    import ctypes
+
+    import torch
+
+    host = [(workloads.s1_frame, workloads.s2_frame, workloads.s3_frame)[i % 3](i, 640, 480)
+            for i in range(24)]
+    frames = torch.from_numpy(np.stack(host)).cuda()
+    F, H, W = frames.shape
+    cfg = _native.FdfConfig(16, 9, nms)
+    out = torch.empty((F * 120_000, 2), dtype=torch.int32, device="cuda")
+    offs = torch.zeros(F + 1, dtype=torch.int64, device="cuda")
+    ctx = _native.Context(0)
+    ctx.lock = __import__("threading").Lock()
+    lib = _native.load()
+    runs = []
+    try:
+        ctx.set_band_rows(8)
+        stream = torch.cuda.current_stream()
+        for _ in range(4):
+            out.fill_(-1)
+            rc = lib.fdf_detect_device(ctx.handle, frames.data_ptr(), F, W, H, W * H,
+                                       ctypes.byref(cfg), out.data_ptr(), out.shape[0],
+                                       offs.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+            _native.check(rc, "fdf_detect_device")
+            torch.cuda.synchronize()
+            o = offs.cpu().numpy().copy()
+            assert o[-1] <= out.shape[0]
+            runs.append((o, out[: o[-1]].cpu().numpy().astype(np.uint32)))
+    finally:
+        ctx.close()
+    for o, p in runs[1:]:
+        assert np.array_equal(o, runs[0][0]) and np.array_equal(p, runs[0][1])
+    o, p = runs[0]
+    for f in range(F):
+        assert np.array_equal(p[o[f]:o[f + 1]], oracle.detect(host[f], 16, 9, nms)), f

@@ -71,7 +71,13 @@ def summarize(st, ntasks_expected):
     waves = {"sweep_end_spread_cycles_p50_p90": [round(float(np.percentile(spread, q)), 0) for q in (50, 90)],
              "spread_over_slowest_sweep_p50": round(float(np.median(spread / np.maximum(rel.max(axis=1), 1))), 3),
              "slowest_wave_share": [round(float(np.mean(rel.argmax(axis=1) == w)), 3) for w in range(4)]}
-    return {"phases_cycles_p50": phases, "waves": waves,
+    # bands running at once (a persistent grid's workgroups run several bands each)
+    ev = np.concatenate([np.stack([s_us, np.ones_like(s_us)], 1), np.stack([e_us, -np.ones_like(e_us)], 1)])
+    ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+    run = np.cumsum(ev[:, 1])
+    dt = np.diff(ev[:, 0], append=ev[-1, 0])
+    conc = {"max": int(run.max()), "time_mean": round(float((run * dt).sum() / max(dt.sum(), 1e-9)), 1)}
+    return {"phases_cycles_p50": phases, "waves": waves, "concurrent_bands": conc,
         "workgroups": int(len(st)), "ntasks": int(ntasks_expected),
         "span_us": round(span, 2),
         "cus_seen": len(first_per_cu),
