@@ -36,7 +36,7 @@ def parse_args(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--settle-seconds", type=float, default=0.0,
+    p.add_argument("--settle-seconds", type=float, default=1.0,
                    help="untimed back-to-back launches before the warm-up steps (sustained clocks)")
     p.add_argument("--frames", type=int, default=512, help="frames per GPU per step")
     p.add_argument("--frames-total", type=int, default=0,
