@@ -27,7 +27,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixels/sec 1920x1080 t=16 n=9 (+NMS) at 1/2/4/8 GPUs; keypoints bit-exact"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
-TIMING_EVERY = 5          # timed regions sample the kernel durations of every 5th launch
+# timed regions sample the kernel durations of every k-th launch, k = timing_every(steps):
+# at least 10 samples when the run has them (each timestamped dispatch costs ~10 us of queue
+# time, profiles/r03/l10_gap_*.json, so not every launch of a long run is timed)
+MIN_TIMED = 10
 NMS_NAMES = {"off": 0, "maxt": 1, "sad": 2}
 
 
@@ -51,11 +54,26 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="budget for the single-thread CPU baseline sample (0 = skip)")
     p.add_argument("--no-extras", action="store_true", help="skip latency/parity extras")
+    p.add_argument("--ranks-share-device", action="store_true",
+                   help="multi-rank runs on a one-GPU box: every rank uses cuda:0, and the "
+                        "barrier and reductions go over gloo (the line composes as on N GPUs)")
+    p.add_argument("--no-strong-leg", action="store_true",
+                   help="N>1: skip extras.config4_strong (BASELINE config 4 as 512 frames in total)")
     p.add_argument("--input", default=os.environ.get("INPUT_FILE", ""),
                    help="an image (PNG/PGM, converted as image 0.24.6 to_luma8) for the "
                         "single-frame GPU and CPU legs, as the reference's bench takes "
                         "INPUT_FILE (benches/benchmark.rs:6-7); the batch stays synthetic")
     return p.parse_args(argv)
+
+
+def timing_every(steps):
+    """Sampling interval of the kernel timing: every launch up to 2 * MIN_TIMED steps, then
+    the largest interval that still samples MIN_TIMED launches (at most every 5th)."""
+    return max(1, min(5, steps // MIN_TIMED))
+
+
+# torch.distributed's reductions run on this device ("cpu" under gloo when ranks share a GPU)
+_REDUCE_DEVICE = None
 
 
 def dist_env():
@@ -121,7 +139,7 @@ def reduce_max(value, world, device):
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_REDUCE_DEVICE or device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -132,7 +150,7 @@ def reduce_sum(value, world, device):
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_REDUCE_DEVICE or device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -335,7 +353,7 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, 
     for _ in range(3):
         fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
     ctx = fast_hip.context(device.index or 0)
-    ctx.set_timing(True, every=TIMING_EVERY)
+    ctx.set_timing(True, every=timing_every(steps))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -493,9 +511,9 @@ def timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, steps, warmup, wo
     torch.cuda.synchronize()
     # HIP events the library's dispatches timestamp on the launch stream (fdf_ctx_set_timing):
     # the detector kernel's own duration, live in the timed region, sampled every
-    # TIMING_EVERY-th launch (each timestamped dispatch costs ~10 us of queue time:
+    # timing_every(steps)-th launch (each timestamped dispatch costs ~10 us of queue time:
     # profiles/r03/l10_gap_*.json)
-    ctx.set_timing(True, every=TIMING_EVERY)
+    ctx.set_timing(True, every=timing_every(steps))
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -509,21 +527,27 @@ def timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, steps, warmup, wo
     return elapsed, det, com
 
 
-def roofline_of(det_ms, com_ms, alg_bytes, call_bytes, traffic):
-    """Roofline of the detector kernel from its per-launch HIP-event durations; `traffic`
-    is load_traffic()'s (bytes, stamp)."""
+def roofline_of(det_ms, com_ms, alg_bytes, in_bytes, traffic):
+    """Roofline of the detector kernel from its per-launch HIP-event durations: `alg_bytes`
+    = W*H + 8K + 4 per frame (SURVEY.md §8d), `in_bytes` = the input pixels alone;
+    `traffic` is load_traffic()'s (bytes, stamp).  Percentiles only from >= MIN_TIMED
+    samples (fewer: the mean alone)."""
     sweep = float(np.mean(det_ms)) if len(det_ms) else float("nan")
     comp = float(np.mean(com_ms)) if len(com_ms) else float("nan")
     achieved = alg_bytes / (sweep * 1e-3) / 1e9
     tbytes, tstamp = traffic
+    enough = len(det_ms) >= MIN_TIMED
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tbytes,
             "traffic_stamp": tstamp,
             "kernel": "fast_sweep_kernel", "kernel_ms_avg": round(sweep, 4),
-            "kernel_ms": percentiles(det_ms), "timed_launches": int(len(det_ms)),
+            "kernel_ms": percentiles(det_ms) if enough else None,
+            "timed_launches": int(len(det_ms)),
             "alg_bytes_per_launch": int(alg_bytes),
-            "compaction_kernel_ms_avg": round(comp, 4), "compaction_kernel_ms": percentiles(com_ms),
-            "call_GBps": round(call_bytes / ((sweep + comp) * 1e-3) / 1e9, 1),
+            "input_bytes_per_launch": int(in_bytes),
+            "frac_input_bytes_only": round(in_bytes / (sweep * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "compaction_kernel_ms_avg": round(comp, 4),
+            "compaction_kernel_ms": percentiles(com_ms) if enough else None,
             "measured_achievable_peak": 6290.0}
 
 
@@ -549,12 +573,20 @@ def main(argv=None):
     world, rank, local = dist_env()
     import torch
 
+    gpu = 0 if args.ranks_share_device else local
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+        global _REDUCE_DEVICE
+        if args.ranks_share_device:
+            # several ranks on one GPU: RCCL wants one rank per device, so the barrier and
+            # the reductions go over gloo on host tensors (the data path has no collective)
+            dist.init_process_group(backend="gloo")
+            _REDUCE_DEVICE = "cpu"
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(gpu)
+    device = torch.device("cuda", gpu)
 
     import workloads
     from feature_detector_fast_amd import Config, NonMaximalSuppression, _native, fast_hip
@@ -576,7 +608,7 @@ def main(argv=None):
     out = torch.empty((cap, 2), dtype=torch.int32, device=device)
     offs = torch.zeros(count + 1, dtype=torch.int64, device=device)
     stream = torch.cuda.current_stream(device)
-    ctx = fast_hip.context(local)
+    ctx = fast_hip.context(gpu)
 
     elapsed, det, com = timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, args.steps,
                                     args.warmup, world, settle=args.settle_seconds)
@@ -597,12 +629,13 @@ def main(argv=None):
     value = pixels / elapsed * args.steps / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # algorithmic bytes of one detector launch: every pixel of every frame read once
-    # (DESIGN.md §5); the whole call adds the output points and frame offsets
-    alg_bytes = count * W * H
-    call_bytes = alg_bytes + 8 * total_kp + 8 * (count + 1)
+    # algorithmic bytes of one detector launch: every pixel of every frame
+    # read once, plus 8 B per output point and a 4 B count per frame -- W*H + 8K + 4 per
+    # frame; the input bytes alone are reported beside it
+    in_bytes = count * W * H
+    alg_bytes = in_bytes + 8 * total_kp + 4 * count
     cfg_key = f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{args.nms}"
-    roofline = roofline_of(det, com, alg_bytes, call_bytes, load_traffic(cfg_key))
+    roofline = roofline_of(det, com, alg_bytes, in_bytes, load_traffic(cfg_key))
 
     extras = {}
     cpu = None
@@ -623,26 +656,30 @@ def main(argv=None):
                    "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
                    "ms_per_step": round(e2 * 1e3 / args.steps, 4),
                    "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
-                   "roofline": roofline_of(d2, c2, alg_bytes, alg_bytes + 8 * kp2 + 8 * (count + 1),
+                   "roofline": roofline_of(d2, c2, in_bytes + 8 * kp2 + 4 * count, in_bytes,
                                            load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
                    "parity": check_parity(oracle, frames, pts2, offs.cpu().numpy(), first, count,
                                           args.threshold, args.count, NMS_NAMES[other], W)}
             extras[f"nms_{other}"] = leg
-        if world > 1 and not strong:
-            # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU
-            f4, c4 = strong_shard(rank, world, 512)
-            cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29)
-            off4 = torch.zeros(c4 + 1, dtype=torch.int64, device=device)
-            e4, d4, _ = timed_steps(fast_hip, ctx, cop4, cfg, out, off4, stream, args.steps,
-                                    args.warmup, world, settle=args.settle_seconds)
-            e4 = reduce_max(e4, world, device)
-            extras["config4_strong"] = {
-                "workload": f"512 {W}x{H} frames in total, {c4} per GPU (rank {rank}), "
-                            f"nms={args.nms}; rotated through {len(cop4)} copies (HBM reads)",
-                "value": round(512 * W * H / e4 * args.steps / 1e6, 1), "unit": "Mpixels/s",
-                "ms_per_step": round(e4 * 1e3 / args.steps, 4), "scaling": "strong",
-                "kernel_ms": percentiles(d4)}
-            del cop4
+    if world > 1 and not strong and not args.no_strong_leg:
+        # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU (run
+        # with --no-extras too: it is the multi-GPU line's own strong-scaling number)
+        f4, c4 = strong_shard(rank, world, 512)
+        cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29)
+        off4 = torch.zeros(c4 + 1, dtype=torch.int64, device=device)
+        e4, d4, _ = timed_steps(fast_hip, ctx, cop4, cfg, out, off4, stream, args.steps,
+                                args.warmup, world, settle=args.settle_seconds)
+        e4 = reduce_max(e4, world, device)
+        kp4 = int(reduce_sum(float(off4[-1].item()), world, device))
+        extras["config4_strong"] = {
+            "workload": f"512 {W}x{H} frames in total, {c4} per GPU (rank {rank}), "
+                        f"nms={args.nms}; rotated through {len(cop4)} copies (HBM reads)",
+            "value": round(512 * W * H / e4 * args.steps / 1e6, 1), "unit": "Mpixels/s",
+            "ms_per_step": round(e4 * 1e3 / args.steps, 4), "scaling": "strong",
+            "frames_total": 512, "keypoints_per_step": kp4,
+            "kernel_ms_avg": round(float(np.mean(d4)), 4) if len(d4) else None,
+            "kernel_ms": percentiles(d4) if len(d4) >= MIN_TIMED else None}
+        del cop4
     if rank == 0 and not args.no_extras:
         # single-frame latency (device-resident frame, one launch, HIP events), on --input
         # when given (the reference's bench image, benches/benchmark.rs:6-16), else S1 frame 0
@@ -706,7 +743,8 @@ def main(argv=None):
                        "threshold": args.threshold, "count": args.count, "nms": args.nms,
                        "hbm_copies": len(copies),
                        "workspace_bytes": ctx.workspace_bytes(),
-                       "parallelism": f"frame-sharded x{world} (no collective)"},
+                       "parallelism": f"frame-sharded x{world} (no collective)",
+                       "ranks_share_device": bool(args.ranks_share_device)},
             "keypoints_per_step": int(kp_total),
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -54,7 +54,8 @@ struct fdf_ctx {
     bool sums_dirty = false;            // a launch failed: re-zero before the next use
     // NMS keypoint density feedback (band height): the compaction writes the last finished
     // launch's pre-NMS keypoint total to host-mapped memory, tagged with its launch number
-    uint64_t* h_stats = nullptr;        // pinned, mapped; *h_stats = seq << 32 | total
+    uint64_t* h_stats = nullptr;        // pinned, mapped; *h_stats = seq << 32 | total;
+                                        // h_stats[1]: the direct output's look-back error word
     uint64_t* d_stats = nullptr;        // its device address
     uint32_t stats_seq = 0;
     struct LaunchInfo { uint32_t seq = 0, t = 0, n = 0, nms = 0, w = 0; double pixels = 0; };
@@ -85,7 +86,13 @@ struct fdf_ctx {
     std::vector<uint8_t> timed_compact;   // per recorded call: 1 if it launched the compaction
     // direct output of small grids (BandParams::direct): look-back descriptors, launch tag
     uint64_t* d_lookback = nullptr;       size_t lookback_n = 0;
+    // band tickets: the device counter (a spare word of d_sums, zeroed with it) has handed out
+    // ticket_next tickets, ntasks per direct launch
+    uint32_t ticket_next = 0;
     uint32_t cus = 0;                     // compute units of the device
+    // workgroups per CU of a detector instance (sweep_occupancy), by configuration
+    struct Occupancy { uint32_t nms, n, lds; bool rgb; uint32_t wg; };
+    std::vector<Occupancy> occupancy;
     // debug builds (FDF_STAMPS set): the last detector launch's workgroup stamps
     uint64_t* d_stamps = nullptr;         size_t stamps_n = 0;
     uint64_t stamps_used = 0;             // words written by the last launch
@@ -93,6 +100,7 @@ struct fdf_ctx {
 
 constexpr size_t kMaxTimedCalls = 4096;
 constexpr uint64_t kDefaultMinTasks = 1024;   // 4 workgroups on each of 256 CUs
+constexpr uint32_t kMaxBandRows = 256;        // fdf_ctx_set_band_rows: the automatic path's range
 
 // process-wide counters: fdf_detect_batch_multi call generations, direct-output launch tags
 std::atomic<uint64_t> g_multi_gen{0};
@@ -242,23 +250,48 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
 // Enqueue detection + compaction over `n_frames` device frames (w, h >= 7) on `stream`,
 // after the context's previous device work (which may have run on another stream: the
 // workspace is shared).
+// The direct output's look-back error word (h_stats[1]): set by a band whose wait ran out.
+volatile uint32_t* lookback_error_word(fdf_ctx* ctx) {
+    return ctx->h_stats ? reinterpret_cast<volatile uint32_t*>(ctx->h_stats + 1) : nullptr;
+}
+
+// Takes (reads and clears) the look-back error word.
+bool take_lookback_error(fdf_ctx* ctx) {
+    volatile uint32_t* e = lookback_error_word(ctx);
+    if (!e || *e == 0) return false;
+    *e = 0;
+    return true;
+}
+
+// Workgroups one CU holds of the detector instance for (nms, n) with `lds` bytes of LDS, from
+// the runtime's occupancy calculator (registers, LDS, waves), cached per configuration.
+uint32_t wg_per_cu(fdf_ctx* ctx, uint32_t nms, uint32_t n, uint32_t lds, bool rgb) {
+    for (const auto& o : ctx->occupancy)
+        if (o.nms == nms && o.n == n && o.lds == lds && o.rgb == rgb) return o.wg;
+    int wg = 0;
+    if (fdfk::sweep_occupancy(nms, n, lds, rgb, &wg) != hipSuccess || wg <= 0)
+        wg = (int)std::min<uint32_t>(4u, fdfk::kSweepMaxLds / std::max(lds, 1u));   // LDS bound only
+    ctx->occupancy.push_back({nms, n, lds, rgb, (uint32_t)wg});
+    return (uint32_t)wg;
+}
+
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream, bool rgb = false) {
     double density = 0.0;
-    if (cfg->nms) {
-        if (!ctx->h_stats) {
-            void* hp = nullptr;
-            void* dp = nullptr;
-            if (hipHostMalloc(&hp, 64, hipHostMallocMapped) == hipSuccess &&
-                hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
-                ctx->h_stats = static_cast<uint64_t*>(hp);
-                ctx->d_stats = static_cast<uint64_t*>(dp);
-                *ctx->h_stats = 0;
-            } else if (hp) {
-                (void)hipHostFree(hp);
-            }
+    if (!ctx->h_stats) {
+        void* hp = nullptr;
+        void* dp = nullptr;
+        if (hipHostMalloc(&hp, 64, hipHostMallocMapped) == hipSuccess &&
+            hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
+            ctx->h_stats = static_cast<uint64_t*>(hp);
+            ctx->d_stats = static_cast<uint64_t*>(dp);
+            std::memset(hp, 0, 64);
+        } else if (hp) {
+            (void)hipHostFree(hp);
         }
+    }
+    if (cfg->nms) {
         if (ctx->h_stats) {
             const uint64_t v = *reinterpret_cast<volatile uint64_t*>(ctx->h_stats);
             const uint32_t seq = (uint32_t)(v >> 32);
@@ -328,15 +361,19 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
                            stream) != hipSuccess)
             return FDF_ERR_DEVICE;
         ctx->sums_dirty = false;
+        ctx->ticket_next = 0;                       // the ticket counter is zero again
     }
     // detection and compaction are two launches: a compaction fused into the detector's last
     // workgroup measured 87 us for one frame against 13 + 12 us (every workgroup's device-scope
     // release is an L2 writeback on gfx950)
     // Small grids write their points directly (look-back, no compaction launch) when every
-    // workgroup is resident at once: 4 per CU (4 waves per SIMD), fewer if LDS-bound
+    // workgroup is resident at once -- by the occupancy calculator for this instance and LDS
+    // size (4 per CU at 4 waves per SIMD) -- so that a band's look-back only waits for bands
+    // running beside it.  (Correctness does not depend on it: bands are numbered by their
+    // start tickets, band_lookback.)
     const fdfk::SweepLayout lay = fdfk::make_sweep_layout(R, nw, cfg->nms);
-    const uint32_t wg_per_cu = std::min<uint32_t>(4u, fdfk::kSweepMaxLds / std::max(lay.total, 1u));
-    bool direct = ntasks <= std::min<uint64_t>(fdfk::kDirectMaxTasks, (uint64_t)ctx->cus * wg_per_cu);
+    const uint32_t wgs = wg_per_cu(ctx, cfg->nms, cfg->count, lay.total, rgb);
+    bool direct = ntasks <= std::min<uint64_t>(fdfk::kDirectMaxTasks, (uint64_t)ctx->cus * wgs);
 #ifdef FDF_DEBUG_BUILD
     if (const char* e = std::getenv("FDF_DIRECT")) direct = direct && std::strtoul(e, nullptr, 0) != 0;
 #endif
@@ -386,6 +423,9 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.out = d_out;
     p.cap = cap;
     p.frame_offsets = d_offsets;
+    p.ticket = ctx->d_sums + 2 * fdfk::kMaxGroupSums + 2;
+    p.ticket_base = ctx->ticket_next;
+    p.lookback_error = ctx->h_stats ? reinterpret_cast<uint32_t*>(ctx->d_stats + 1) : nullptr;
     if (direct) {
         // a (re)allocated buffer is zeroed: recycled device memory can hold descriptors of
         // another context's launches.  Launch tags are unique in the process as well.
@@ -442,6 +482,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
+    if (direct) ctx->ticket_next += (uint32_t)ntasks;   // the launch takes one per workgroup
     if (!direct && fdfk::launch_compact(c, stream, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr) !=
                        hipSuccess) {
         ctx->sums_dirty = true;
@@ -535,6 +576,20 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                                   hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return FDF_ERR_DEVICE;
+    if (take_lookback_error(ctx)) {
+        // a direct-output band's look-back ran out (band_lookback): the offsets and points of
+        // its frame on are not written; the slots and counts are, so the compaction rebuilds
+        // both from them
+        fdfk::CompactParams c = ctx->last_compact;
+        c.kp_stats = nullptr;
+        c.group_sums = nullptr;
+        e = fdfk::launch_compact(c, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(offs, ctx->d_offsets, sizeof(uint64_t) * (n_frames + 1ull),
+                               hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return FDF_ERR_DEVICE;
+    }
     const uint64_t total = offs[n_frames];
     if (total > ctx->out_points) {
         // grow the output and compact again (the offsets do not change)
@@ -755,7 +810,7 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
 }
 
 int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows) {
-    if (!ctx) return FDF_ERR_ARG;
+    if (!ctx || rows > kMaxBandRows) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->band_rows = rows;
     return FDF_OK;
@@ -904,6 +959,9 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);   // NULL = the HIP null stream
     std::lock_guard<std::mutex> lock(ctx->mu);
     DeviceGuard guard(ctx->device);
+    // an earlier asynchronous direct-output launch of this context had a look-back wait run
+    // out (band_lookback; never seen in practice): its output was incomplete -- reported once
+    if (take_lookback_error(ctx)) return FDF_ERR_DEVICE;
     if (empty) {
         return hipMemsetAsync(d_frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull), s) ==
                        hipSuccess
@@ -933,6 +991,9 @@ int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_fram
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lock(ctx->mu);
     DeviceGuard guard(ctx->device);
+    // an earlier asynchronous direct-output launch of this context had a look-back wait run
+    // out (band_lookback; never seen in practice): its output was incomplete -- reported once
+    if (take_lookback_error(ctx)) return FDF_ERR_DEVICE;
     if (empty) {
         return hipMemsetAsync(d_frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull), s) ==
                        hipSuccess

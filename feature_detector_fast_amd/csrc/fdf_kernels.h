@@ -197,13 +197,23 @@ struct BandParams {
     uint2* out;                  // direct: the caller's points, `cap` of them
     uint64_t cap;
     uint64_t* frame_offsets;     // direct: frames + 1 entries
+    // Direct output: a workgroup's band is its ticket (a device counter taken when it starts,
+    // less this launch's first ticket), so bands are swept in the order workgroups start and
+    // a band's look-back only ever waits on bands that started before it -- no residency
+    // assumption.  Each launch takes exactly ntasks tickets; the host keeps the running base.
+    uint32_t* ticket;
+    uint32_t ticket_base;
+    // Direct output: set when a look-back wait ran out (host-mapped; the band then publishes
+    // no prefix and writes no points, and the host recovers from the slots: fdf_api.cpp)
+    uint32_t* lookback_error;
 };
 constexpr uint64_t kLbAggregate = 1ull << 30;   // value = the band's own keypoint count
 constexpr uint64_t kLbPrefix = 1ull << 31;      // value = keypoints of bands 0 .. this one
 constexpr uint64_t kLbValue = kLbAggregate - 1;
-// Direct output only when the whole grid is resident at once (look-back waits on earlier
-// bands only, and they must already be running): up to this many workgroups, within
-// the CU count times the workgroups one CU holds (host side, fdf_api.cpp).
+constexpr uint64_t kLbNoBase = ~0ull;           // band_lookback's result after a timeout
+// Direct output pays off when the whole grid is resident at once (a band's look-back then
+// waits only for bands running beside it): up to this many workgroups, within the CU count
+// times the workgroups one CU holds by the kernel's occupancy (host side, fdf_api.cpp).
 constexpr uint32_t kDirectMaxTasks = 1024;
 
 // start / stop (optional): events the dispatch itself timestamps (hipExtLaunchKernelGGL), so
@@ -212,6 +222,10 @@ hipError_t launch_compact(const CompactParams& c, hipStream_t stream, hipEvent_t
                           hipEvent_t stop = nullptr);
 hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
                         hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// Workgroups of the detector instance (nms, n; grey or RGB) one CU holds at once with
+// `lds_bytes` of dynamic LDS (the runtime's occupancy calculator: registers, LDS, waves).
+hipError_t sweep_occupancy(uint32_t nms, uint32_t n, uint32_t lds_bytes, bool rgb, int* wg_per_cu);
+hipError_t sweep_occupancy_rgb(uint32_t nms, uint32_t n, uint32_t lds_bytes, int* wg_per_cu);
 // RGB8 frames (3 bytes per pixel, frame_stride in bytes), luma converted on load
 hipError_t launch_sweep_rgb(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
                             hipEvent_t start = nullptr, hipEvent_t stop = nullptr);

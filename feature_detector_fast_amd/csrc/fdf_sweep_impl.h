@@ -1044,10 +1044,13 @@ __device__ void band_nms_dense(uint32_t* bitmap, uint32_t rows, uint32_t nw, uin
 // at once, then wave 0 reads the descriptors of the 64 bands before it in one load per lane
 // (agent-scope relaxed atomics: sc1 loads and stores, each descriptor one 8-byte word, so a
 // flag and its value can never be seen apart), sums the aggregates down to the nearest band
-// that has published its inclusive prefix, and publishes its own prefix.  Bands only wait
-// for earlier bands, and the host enables this only when the whole grid is resident, so
-// every wait ends; a wait is still bounded (it never takes more than a few microseconds;
-// the bound only keeps a broken grid from hanging the GPU).  Returns the base in every thread.
+// that has published its inclusive prefix, and publishes its own prefix.  A band's number is
+// its workgroup's start ticket (fast_sweep_kernel), so it only waits for bands whose
+// workgroups started before it -- running or done -- and every wait ends without assuming
+// the grid is resident.  A wait is still bounded (~30 ms; a band waits microseconds): past
+// the bound the band publishes no prefix, sets P.lookback_error and returns kLbNoBase, and
+// the host recovers the output from the slots (fdf_api.cpp).  Returns the base in every
+// thread.
 __device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t total,
                                   uint64_t* s_base) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1059,6 +1062,7 @@ __device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t t
         uint64_t excl = 0;
         int64_t j = (int64_t)task - 1;
         uint32_t polls = 0;
+        bool timed_out = false;                      // wave-uniform (polls is)
         while (j >= 0) {
             const int64_t k = j - (int64_t)lane;
             // bands before band 0 read as an inclusive prefix of 0
@@ -1070,7 +1074,10 @@ __device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t t
             const uint32_t stop = pref ? (uint32_t)__builtin_ctzll(pref) : 63u;
             const uint64_t need = stop == 63u ? ~0ull : (2ull << stop) - 1ull;
             if ((wave_ballot(ok) & need) != need) {
-                if (++polls > (1u << 20)) break;
+                if (++polls > (1u << 20)) {
+                    timed_out = true;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
@@ -1082,9 +1089,17 @@ __device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t t
             j -= 64;
         }
         if (lane == 0) {
-            __hip_atomic_store(&P.lookback[task], ep | kLbPrefix | ((excl + total) & kLbValue),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *s_base = excl;
+            if (timed_out) {
+                // no prefix: later bands chained on it time out the same way
+                if (P.lookback_error)
+                    __hip_atomic_fetch_or(P.lookback_error, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                *s_base = kLbNoBase;
+            } else {
+                __hip_atomic_store(&P.lookback[task], ep | kLbPrefix | ((excl + total) & kLbValue),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *s_base = excl;
+            }
         }
     }
     __syncthreads();
@@ -1310,15 +1325,17 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     uint8_t* slot = P.slots + (uint64_t)task * P.slot_bytes;
     const bool listed = total <= P.slot_bytes / 8;
     uint64_t dbase = 0;
-    if (P.direct) {
+    bool direct = P.direct != 0;
+    if (direct) {
         dbase = band_lookback(P, task, total, reinterpret_cast<uint64_t*>(smem_raw + L.misc + 32));
         if constexpr (kDebugBuild) ph[3] = __builtin_amdgcn_s_memtime();   // look-back done
-        if (tid == 0) {
-            if (band == 0) P.frame_offsets[frame] = dbase;
-            if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = dbase + total;
-        }
+        direct = dbase != kLbNoBase;                  // timed out: the slot only
     }
-    if (listed || P.direct) {
+    if (direct && tid == 0) {
+        if (band == 0) P.frame_offsets[frame] = dbase;
+        if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = dbase + total;
+    }
+    if (listed || direct) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
         uint32_t o = before;
         for (uint32_t g0 = gb; g0 < ge; g0 += 64) {
@@ -1342,7 +1359,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
                 }
                 const uint2 pt = make_uint2(xb + bit, y0 + r);
                 if (listed) pts[idx] = pt;
-                if (P.direct && dbase + idx < P.cap) P.out[dbase + idx] = pt;
+                if (direct && dbase + idx < P.cap) P.out[dbase + idx] = pt;
                 ++idx;
             }
         }
@@ -1367,7 +1384,17 @@ void fast_sweep_kernel(BandParams P) {
             r0 = __builtin_amdgcn_s_memrealtime();
         }
     }
-    const uint32_t task = band_task(P);
+    uint32_t task;
+    if (P.direct) {
+        // the band is the workgroup's start ticket (see band_lookback), raster order
+        uint32_t* s_ticket = reinterpret_cast<uint32_t*>(
+            smem_raw + make_sweep_layout(P.rows, P.words_per_row, NMS).misc + 40);
+        if (threadIdx.x == 0) *s_ticket = atomicAdd(P.ticket, 1u) - P.ticket_base;
+        __syncthreads();
+        task = *s_ticket;
+    } else {
+        task = band_task(P);
+    }
     uint64_t ph[4] = {0, 0, 0, 0};
     const uint32_t total = sweep_band<NMS, N>(P, smem_raw, task, ph);
     const uint32_t tid = threadIdx.x;
@@ -1417,15 +1444,25 @@ static SweepKernelFn pick_sweep_n(uint32_t n) {
     }
 }
 
+static SweepKernelFn pick_sweep(uint32_t nms, uint32_t n) {
+    switch (nms) {
+        case kNmsOff: return pick_sweep_n<kNmsOff>(n);
+        case kNmsMaxThreshold: return pick_sweep_n<kNmsMaxThreshold>(n);
+        case kNmsSumAbsolute: return pick_sweep_n<kNmsSumAbsolute>(n);
+        default: return nullptr;
+    }
+}
+
+hipError_t occupancy(uint32_t nms, uint32_t n, uint32_t lds_bytes, int* wg_per_cu) {
+    SweepKernelFn fn = pick_sweep(nms, n);
+    if (!fn || !wg_per_cu) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_per_cu, reinterpret_cast<const void*>(fn),
+                                                        kThreads, lds_bytes);
+}
+
 hipError_t launch(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
                   hipEvent_t start, hipEvent_t stop) {
-    SweepKernelFn fn = nullptr;
-    switch (nms) {
-        case kNmsOff: fn = pick_sweep_n<kNmsOff>(n); break;
-        case kNmsMaxThreshold: fn = pick_sweep_n<kNmsMaxThreshold>(n); break;
-        case kNmsSumAbsolute: fn = pick_sweep_n<kNmsSumAbsolute>(n); break;
-        default: break;
-    }
+    SweepKernelFn fn = pick_sweep(nms, n);
     if (!fn) return hipErrorInvalidValue;
     const SweepLayout L = make_sweep_layout(p.rows, p.words_per_row, nms);
     if (L.total > kSweepMaxLds) return hipErrorInvalidValue;

@@ -10,4 +10,7 @@ hipError_t launch_sweep_rgb(const BandParams& p, uint32_t nms, uint32_t n, hipSt
                         hipEvent_t start, hipEvent_t stop) {
     return rgb::launch(p, nms, n, stream, start, stop);
 }
+hipError_t sweep_occupancy_rgb(uint32_t nms, uint32_t n, uint32_t lds_bytes, int* wg_per_cu) {
+    return rgb::occupancy(nms, n, lds_bytes, wg_per_cu);
+}
 }  // namespace fdfk

@@ -112,7 +112,8 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
  * rows (rounded up to the geometry's sub-band multiple, capped by what the workgroup's LDS
  * holds, 160 KB); 0 restores the automatic choice (LDS budget, grid size, and for NMS the
  * keypoint density of the previous launch).  The keypoints are the same at every height;
- * tests use it to cross the band NMS pass's LDS / spill / dense tiers. */
+ * tests use it to cross the band NMS pass's LDS / spill / dense tiers.  rows > 256 (outside
+ * the automatic choice's range): FDF_ERR_ARG. */
 int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows);
 
 /* Device bytes the context's workspace holds now (host-API staging and output, per-band
@@ -203,8 +204,14 @@ int fdf_fetch_last_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, fdf_point* out, s
  * and d_frame_offsets[n_frames] the total, even when the total exceeds `cap` (points with
  * index >= cap are not written).  Argument and shape errors are returned synchronously.
  * The context's workspace is reused by each call: a call on another stream than the
- * context's previous call first waits (on the device) for that call's work.  Frames before the last may be read up to 15 bytes
- * past their end (inside the batch allocation); the last frame is read exactly.
+ * context's previous call first waits (on the device) for that call's work.  Frames may be
+ * spaced by any frame_stride_bytes >= width * height (the gap bytes are never centres or
+ * circle pixels); frames before the last may be read up to 15 bytes past their end (inside
+ * the batch allocation), the last frame is read exactly.  FDF_ERR_DEVICE is also returned,
+ * once, by the call after an asynchronous launch whose output could not be completed (a
+ * grid small enough to write its points directly, whose look-back wait ran out: the
+ * bounded wait that keeps a faulty device from hanging; the host entry points recover such
+ * a launch by themselves).
  */
 int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
                       uint32_t width, uint32_t height, uint64_t frame_stride_bytes,

@@ -11,10 +11,12 @@
 #   ablate|NAME|ARGS                   tools/ablate.py ARGS on the debug build -> NAME.json
 #   pmc|NAME|VARIANT|ARGS              SQ / TCC counter passes of one variant (debug build)
 #   pmcv|NAME|VARIANTS|ARGS            one instruction-count pass per variant (debug build)
+#   pmct|NAME|VARIANTS|ARGS            L2 hit/miss + FETCH_SIZE (+ VALU/VMEM) per variant (debug build)
 #   stamps|NAME|ARGS                   tools/stamps.py ARGS (debug build) -> NAME.json
 #   profile|TAG|ARGS                   tools/profile_round.sh TAG ARGS (kernel stats + traffic)
 #   single|NAME                        single-frame latency + kernel traces (off, max-t)
 #   py|NAME|SCRIPT ARGS                python3 SCRIPT ARGS             -> NAME.json
+#   trace|NAME|SCRIPT ARGS[|LAST]      rocprofv3 kernel trace of a script -> NAME.json (overlap, gaps)
 set -o pipefail
 O=gpurun_out/${1:?out}; shift
 mkdir -p "$O"
@@ -74,6 +76,23 @@ for STEP in "$@"; do
       done
       cat "$O/$A1.txt"
       rm -rf "$D" ;;
+    pmct)
+      # memory-side traffic per variant (comma-separated): L2 hits / misses and FETCH_SIZE,
+      # each counter set in its own rocprofv3 run
+      D="$O/$A1"; mkdir -p "$D"; : > "$O/$A1.txt"
+      IFS=',' read -r -a VS <<< "$A2"
+      for v in "${VS[@]}"; do
+        t=$(echo "$v" | tr ':.' '__')
+        k=0
+        for set in "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE"; do
+          k=$((k+1))
+          FDF_LIB_PATH=$DEBUG_LIB timeout -s KILL 120 rocprofv3 --pmc $set -d "$D/${t}_$k" -o p --output-format csv -- \
+              python3 tools/ablate.py --rounds 1 --iters 2 $A3 --variants "$v" > "$D/${t}_$k.log" 2>&1 || fail "$STEP $v $k" "$D/${t}_$k.log"
+        done
+        echo "$v $(python3 tools/pmc_summary.py "$D/${t}_1" "$D/${t}_2" "$D/${t}_3" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(json.dumps({k: round(v) for k, v in d.items() if not k.startswith("_")}))')" >> "$O/$A1.txt"
+      done
+      cat "$O/$A1.txt"
+      rm -rf "$D" ;;
     stamps)
       FDF_LIB_PATH=$DEBUG_LIB timeout -k 10 400 python3 tools/stamps.py $A2 > "$O/$A1.json" 2> "$L" || fail "$STEP" "$L"
       python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['by_frames']; [print(f, {k: v[k] for k in ('span_us','ramp_us','tail_us_p90_to_last','wg_us_p5_p50_p95','busy_fraction','clock_mhz_p50','event_ms_p50','workgroups','phases_cycles_p50')}) for f, v in d.items()]" "$O/$A1.json" ;;
@@ -89,6 +108,11 @@ for STEP in "$@"; do
     py)
       timeout -k 10 600 python3 $A2 > "$O/$A1.json" 2> "$L" || fail "$STEP" "$L"
       tail -c 2000 "$O/$A1.json"; echo ;;
+    trace)
+      # kernel trace of a python script, then the kernels' overlap / gaps (tools/trace_overlap.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/$A1" -o p -- python3 $A2 > "$O/$A1.out" 2> "$L" || fail "$STEP" "$L"
+      python3 tools/trace_overlap.py "$O/$A1" --last ${A3:-200} > "$O/$A1.json" || fail "$STEP overlap" "$O/$A1.json"
+      cat "$O/$A1.json"; rm -rf "$O/$A1" ;;
     *)
       echo "unknown step kind: $KIND"; exit 2 ;;
   esac

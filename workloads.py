@@ -94,12 +94,22 @@ def s3_frame(seed, w=1920, h=1080):
 
 # ---- inputs given by file (the reference's INPUT_FILE, tests/compare.rs:24-33) ---------------
 
+# PIL modes whose conversion to RGB8 is the same as image 0.24's to_rgb8 (8-bit channels:
+# grey is replicated, alpha dropped, a palette looked up).  16-bit and float images are scaled
+# by image 0.24 and clipped by PIL's convert('RGB'), so they are refused rather than detected
+# on different luma.
+_RGB8_MODES = ("1", "L", "LA", "P", "PA", "RGB", "RGBA", "RGBX")
+
+
 def load_rgb(path):
     """An image file as RGB8 (H, W, 3), as `image::open(..).to_rgb8()` (tests/compare.rs:29-31).
-    PNG / PGM / anything PIL reads; a grey file becomes r = g = b."""
+    PNG / PGM / anything PIL reads with 8-bit channels; a grey file becomes r = g = b."""
     from PIL import Image
 
     with Image.open(path) as im:
+        if im.mode not in _RGB8_MODES:
+            raise ValueError(f"{path}: PIL mode {im.mode!r} is not an 8-bit-per-channel image; "
+                             "its conversion to RGB8 would differ from image 0.24's to_rgb8")
         return np.asarray(im.convert("RGB")).copy()
 
 
