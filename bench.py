@@ -1,17 +1,21 @@
 """Throughput benchmark of the HIP FAST detector (driver contract: one JSON line on rank 0).
 
-A step = one launch of the fused detector over a device-resident batch of synthetic 1080p
-frames (S1 "tiled media", workloads.py) per GPU, t=16 n=9 with max-t NMS (BASELINE.json
-config 4's per-frame work; weak scaling: every rank owns its own batch, no collective on
-the data path).  Inputs are already in HBM when the timed region starts.
+A step = one fdf_detect_device call (detector + compaction) over a device-resident batch of
+synthetic 1080p frames (S1 "tiled media", workloads.py) per GPU, t=16 n=9 with max-t NMS
+(BASELINE.json config 4's per-frame work; weak scaling: every rank owns its own batch, no
+collective on the data path).  Inputs are already in HBM when the timed region starts.
+Step k runs on launch lane k % L (fast_hip.Lanes, --lanes, default 3): each lane is a
+context with its own HIP stream, so consecutive calls overlap on the GPU the way a caller
+streaming batches through the public API would run them (extras.single_lane keeps the
+one-stream protocol of rounds 1-3).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames B] [--nms off|maxt|sad]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Besides the headline value the line carries: the roofline of the detector kernel (HIP
-events on the launch stream; algorithmic bytes = W*H + 8*K + 4 per frame),
-single-frame latencies, a parity check of sampled frames against the CPU oracle, and the
-CPU baseline (the AVX2 port of the reference path, oracle/fast_avx2.cpp, rank 0, N=1).
+Besides the headline value the line carries: the roofline of the detector (HIP events on the
+lane streams; algorithmic bytes = W*H + 8*K + 4 per frame), single-frame
+latencies, a parity check of sampled frames against the CPU oracle, and the CPU baseline
+(the AVX2 port of the reference path, oracle/fast_avx2.cpp, rank 0, N=1).
 """
 import argparse
 import json
@@ -54,6 +58,9 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="budget for the single-thread CPU baseline sample (0 = skip)")
     p.add_argument("--no-extras", action="store_true", help="skip latency/parity extras")
+    p.add_argument("--lanes", type=int, default=3,
+                   help="launch lanes: step k runs on lane k %% L, each lane a context with its "
+                        "own HIP stream and no dependency between lanes (fast_hip.Lanes)")
     p.add_argument("--ranks-share-device", action="store_true",
                    help="multi-rank runs on a one-GPU box: every rank uses cuda:0, and the "
                         "barrier and reductions go over gloo (the line composes as on N GPUs)")
@@ -335,56 +342,47 @@ def host_latency(fast_hip, _native, frame, cfgs, samples=50):
     return res
 
 
-def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, out, stream, device,
-               oracle_detect, frames=128, steps=10, settle=0.0):
+def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device, oracle_detect,
+               frames=128, steps=10, warmup=3, settle=0.0):
     """BASELINE.json config 5 on this GPU: 3840x2160 S1 frames, t=8 n=12 (3-of-4 cardinal
-    pre-filter), SAD NMS; 128 frames = 1.06 GB, the same bytes per launch as config 4."""
-    import torch
-
+    pre-filter), SAD NMS; 128 frames = 1.06 GB, the same bytes per launch as config 4.  Same
+    protocol as the headline (timed_steps over `lanes`), plus one lane for the isolated
+    kernel."""
     W, H = 3840, 2160
     batch = workloads.s1_frames_torch(0, frames, W, H, device=device)
-    offs = torch.zeros(frames + 1, dtype=torch.int64, device=device)
     cfg = Config(8, 12, NonMaximalSuppression.SumAbsolute)
-    t_end = time.perf_counter() + settle          # sustained clocks first (see timed_steps)
-    while time.perf_counter() < t_end:
-        for _ in range(10):
-            fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
-        torch.cuda.synchronize()
-    for _ in range(3):
-        fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
-    ctx = fast_hip.context(device.index or 0)
-    ctx.set_timing(True, every=timing_every(steps))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    calls, sweep_ms, compact_ms = ctx.timing()
-    ctx.set_timing(False)
-    kernel_ms = sweep_ms / max(calls, 1)
+    bufs = LaneBufs(len(lanes), frames * 120_000, frames, device)
+    t = timed_steps(fast_hip, lanes, bufs, [batch], cfg, steps, warmup, 1, settle=settle)
+    lanes1 = fast_hip.Lanes(1, device.index or 0)
+    buf1 = LaneBufs.__new__(LaneBufs)
+    buf1.out, buf1.offs = bufs.out[:1], bufs.offs[:1]
+    t1 = timed_steps(fast_hip, lanes1, buf1, [batch], cfg, steps, warmup, 1)
     alg = frames * W * H
-    # parity outside the timed region: one more launch must repeat the last one exactly, and
-    # frame 0 and the densest frame must equal the CPU oracle
-    total = int(offs[-1].item())
-    o1 = offs.cpu().numpy().copy()
-    p1 = out[: min(total, out.shape[0])].cpu().numpy().copy()
-    fast_hip.detect_device(batch, cfg, out, offs, stream=stream)
-    torch.cuda.synchronize()
-    repeat_ok = bool(np.array_equal(offs.cpu().numpy(), o1)) and bool(
-        np.array_equal(out[: len(p1)].cpu().numpy(), p1))
+    # parity outside the timed regions: every lane's last result equals the one-lane run's,
+    # and frame 0 and the densest frame equal the CPU oracle
+    o1 = bufs.offs[0].cpu().numpy().copy()
+    total = int(o1[-1])
+    p1 = bufs.out[0][: min(total, bufs.out[0].shape[0])].cpu().numpy().copy()
+    repeat_ok = all(bool(np.array_equal(bufs.offs[i].cpu().numpy(), o1)) and bool(
+        np.array_equal(bufs.out[i][: len(p1)].cpu().numpy(), p1)) for i in range(len(lanes)))
     checked = sorted({0, int(np.argmax(np.diff(o1)))})
     exact = all(np.array_equal(p1[o1[f]:o1[f + 1]].astype(np.uint32),
                                oracle_detect(batch[f].cpu().numpy(), 8, 12, 2)) for f in checked)
     res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad",
-           "Mpix_s": round(alg * steps / elapsed / 1e6, 1),
-           "ms_per_step": round(elapsed * 1e3 / steps, 4),
-           "kernel_ms_avg": round(kernel_ms, 4),
-           "compaction_kernel_ms_avg": round(compact_ms / max(calls, 1), 4),
-           "roofline_frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "Mpix_s": round(alg * steps / t.elapsed / 1e6, 1),
+           "ms_per_step": round(t.elapsed * 1e3 / steps, 4),
+           "lanes": t.lanes,
+           "kernel_ms_avg": round(t.span_ms / steps, 4),
+           "launch_ms_avg": round(float(np.mean(t.det)), 4) if len(t.det) else None,
+           "roofline_frac": round(alg / (t.span_ms / steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "single_lane": {"ms_per_step": round(t1.elapsed * 1e3 / steps, 4),
+                           "kernel_ms_avg": round(float(np.mean(t1.det)), 4) if len(t1.det) else None,
+                           "compaction_kernel_ms_avg": round(float(np.mean(t1.com)), 4) if len(t1.com) else None,
+                           "roofline_frac": round(alg / (float(np.mean(t1.det)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                           if len(t1.det) else None},
            "keypoints_per_step": total,
-           "parity": {"oracle_frames": checked, "bit_exact": exact, "repeat_identical": repeat_ok}}
-    del batch
+           "parity": {"oracle_frames": checked, "bit_exact": exact, "lanes_identical": repeat_ok}}
+    del batch, bufs
     return res
 
 
@@ -490,64 +488,117 @@ def make_batch(workloads, first, count, W, H, device, min_bytes=0):
     return copies
 
 
-def timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, steps, warmup, world, settle=0.0):
+class LaneBufs:
+    """Each lane's own output buffers (a lane's call may still run while the next lane's
+    writes): `cap` points and count + 1 offsets per lane."""
+
+    def __init__(self, n, cap, count, device):
+        import torch
+
+        self.out = [torch.empty((cap, 2), dtype=torch.int32, device=device) for _ in range(n)]
+        self.offs = [torch.zeros(count + 1, dtype=torch.int64, device=device) for _ in range(n)]
+
+
+class Timed:
+    """One timed region: wall seconds between barriers + synchronizes, the GPU span of its
+    launches from HIP events (lane streams wait on a start event, each records an end event),
+    the per-launch detector / compaction durations the library's dispatches timestamped, and
+    the lane that ran the last step (its buffers hold the last result)."""
+
+    def __init__(self, elapsed, span_ms, det, com, last, steps, lanes):
+        self.elapsed, self.span_ms, self.det, self.com = elapsed, span_ms, det, com
+        self.last, self.steps, self.lanes = last, steps, lanes
+
+
+def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle=0.0):
     """W warm-up steps, then K timed steps between barriers + synchronizes; one step = one
-    fdf_detect_device launch over a batch.  Returns (wall seconds, per-launch detector ms,
-    per-launch compaction ms).  `settle` > 0: before the warm-up steps, the same launches back
-    to back for that many seconds (untimed), so the timed steps run at the GPU's sustained
-    clocks -- a cold GPU's launches speed up over the first ~30 ms of load."""
+    fdf_detect_device call over a batch, step k on lane k % L (fast_hip.Lanes: a context and
+    its own HIP stream per lane, no dependency between lanes, so a call's detector runs beside
+    the previous calls' last workgroups and compaction).  `settle` > 0: before the warm-up
+    steps, the same launches back to back for that many seconds (untimed), so the timed steps
+    run at the GPU's sustained clocks -- a cold GPU's launches speed up over the first
+    ~30 ms of load."""
     import torch
+
+    n = len(lanes)
+
+    def call(k):
+        lanes.detect_device(k, copies[k % len(copies)], cfg, bufs.out[k % n], bufs.offs[k % n],
+                            after_current=False)
 
     if settle > 0:
         t_end = time.perf_counter() + settle
         k = 0
         while time.perf_counter() < t_end:
             for _ in range(20):
-                fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+                call(k)
                 k += 1
             torch.cuda.synchronize()
     for k in range(warmup):
-        fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+        call(k)
     torch.cuda.synchronize()
-    # HIP events the library's dispatches timestamp on the launch stream (fdf_ctx_set_timing):
-    # the detector kernel's own duration, live in the timed region, sampled every
-    # timing_every(steps)-th launch (each timestamped dispatch costs ~10 us of queue time:
-    # profiles/r03/l10_gap_*.json)
-    ctx.set_timing(True, every=timing_every(steps))
+    # HIP events the library's dispatches timestamp on each lane's stream (fdf_ctx_set_timing):
+    # every launch's own duration, sampled every timing_every-th call of a lane (each
+    # timestamped dispatch costs ~10 us of queue time: profiles/r03/l10_gap_*.json)
+    for ctx in lanes.ctxs:
+        ctx.set_timing(True, every=timing_every(max(1, steps // n)))
+    start = torch.cuda.Event(enable_timing=True)
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    start.record(torch.cuda.current_stream())
+    for i in range(n):
+        lanes.stream(i).wait_event(start)
     for k in range(steps):
-        fast_hip.detect_device(copies[k % len(copies)], cfg, out, offs, stream=stream)
+        call(k)
+    for i in range(n):
+        ends[i].record(lanes.stream(i))
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
-    det, com = ctx.timing_samples()
-    ctx.set_timing(False)
-    return elapsed, det, com
+    span_ms = max(start.elapsed_time(e) for e in ends)
+    det, com = [], []
+    for ctx in lanes.ctxs:
+        d, c = ctx.timing_samples()
+        det.extend(d.tolist())
+        com.extend(c.tolist())
+        ctx.set_timing(False)
+    return Timed(elapsed, span_ms, det, com, (steps - 1) % n, steps, n)
 
 
-def roofline_of(det_ms, com_ms, alg_bytes, in_bytes, traffic):
-    """Roofline of the detector kernel from its per-launch HIP-event durations: `alg_bytes`
-    = W*H + 8K + 4 per frame (SURVEY.md §8d), `in_bytes` = the input pixels alone;
-    `traffic` is load_traffic()'s (bytes, stamp).  Percentiles only from >= MIN_TIMED
-    samples (fewer: the mean alone)."""
-    sweep = float(np.mean(det_ms)) if len(det_ms) else float("nan")
-    comp = float(np.mean(com_ms)) if len(com_ms) else float("nan")
-    achieved = alg_bytes / (sweep * 1e-3) / 1e9
+def roofline_of(t, alg_bytes, in_bytes, traffic):
+    """Roofline of the detector from a timed region `t`: `alg_bytes` = W*H + 8K + 4 per
+    frame, `in_bytes` = the input pixels alone; `traffic` is
+    load_traffic()'s (bytes, stamp).
+      kernel_ms_avg: the detector's GPU time per launch -- the HIP-event span of the timed
+        region's launches / launches.  With L > 1 lanes the launches overlap (each one's
+        own duration covers the others' beside it), so the span is what a launch costs the
+        GPU; with one lane it is each launch's duration plus its compaction and the gaps.
+      launch_ms_avg: the mean of the launches' own HIP-event durations (the isolated
+        kernel's duration with one lane; with L lanes ~L launches share the GPU in it).
+    Percentiles only from >= MIN_TIMED samples (fewer: the mean alone)."""
+    per_launch = t.span_ms / t.steps
+    launch = float(np.mean(t.det)) if len(t.det) else float("nan")
+    comp = float(np.mean(t.com)) if len(t.com) else float("nan")
+    achieved = alg_bytes / (per_launch * 1e-3) / 1e9
     tbytes, tstamp = traffic
-    enough = len(det_ms) >= MIN_TIMED
+    enough = len(t.det) >= MIN_TIMED
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tbytes,
             "traffic_stamp": tstamp,
-            "kernel": "fast_sweep_kernel", "kernel_ms_avg": round(sweep, 4),
-            "kernel_ms": percentiles(det_ms) if enough else None,
-            "timed_launches": int(len(det_ms)),
+            "kernel": "fast_sweep_kernel", "kernel_ms_avg": round(per_launch, 4),
+            "kernel_ms_basis": f"HIP-event span of {t.steps} launches on {t.lanes} lane stream(s) / launches",
+            "lanes": t.lanes,
+            "launch_ms_avg": round(launch, 4),
+            "launch_ms": percentiles(t.det) if enough else None,
+            "launches_in_flight_avg": round(launch / per_launch, 3) if per_launch > 0 else None,
+            "timed_launches": int(len(t.det)),
             "alg_bytes_per_launch": int(alg_bytes),
             "input_bytes_per_launch": int(in_bytes),
-            "frac_input_bytes_only": round(in_bytes / (sweep * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_input_bytes_only": round(in_bytes / (per_launch * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "compaction_kernel_ms_avg": round(comp, 4),
-            "compaction_kernel_ms": percentiles(com_ms) if enough else None,
+            "compaction_kernel_ms": percentiles(t.com) if enough else None,
             "measured_achievable_peak": 6290.0}
 
 
@@ -605,23 +656,27 @@ def main(argv=None):
     copies = make_batch(workloads, first, count, W, H, device, min_bytes=1 << 29)
     frames = copies[0]
     cap = max(count, 1) * 200_000
-    out = torch.empty((cap, 2), dtype=torch.int32, device=device)
-    offs = torch.zeros(count + 1, dtype=torch.int64, device=device)
     stream = torch.cuda.current_stream(device)
-    ctx = fast_hip.context(gpu)
+    lanes = fast_hip.Lanes(args.lanes, gpu)
+    bufs = LaneBufs(len(lanes), cap, count, device)
+    ctx = lanes.ctxs[0]
+    # lane 0's buffers serve the one-stream extras below
+    out, offs = bufs.out[0], bufs.offs[0]
 
-    elapsed, det, com = timed_steps(fast_hip, ctx, copies, cfg, out, offs, stream, args.steps,
-                                    args.warmup, world, settle=args.settle_seconds)
-    elapsed = reduce_max(elapsed, world, device)
-    total_kp = int(offs[-1].item())
-    offsets = offs.cpu().numpy()
+    tm = timed_steps(fast_hip, lanes, bufs, copies, cfg, args.steps, args.warmup, world,
+                     settle=args.settle_seconds)
+    elapsed = reduce_max(tm.elapsed, world, device)
+    total_kp = int(bufs.offs[tm.last][-1].item())
+    offsets = bufs.offs[tm.last].cpu().numpy()
 
     # ---- parity of sampled frames against the CPU oracle (outside the timed region)
     parity = {}
     if not args.no_extras:
-        pts = out[: min(total_kp, cap)].cpu().numpy().astype(np.uint32)
+        pts = bufs.out[tm.last][: min(total_kp, cap)].cpu().numpy().astype(np.uint32)
         parity = check_parity(oracle, frames, pts, offsets, first, count, args.threshold,
                               args.count, nms, W)
+        parity["lanes_identical"] = all(
+            bool(torch.equal(bufs.offs[i], bufs.offs[tm.last])) for i in range(len(lanes)))
 
     frames_total = reduce_sum(float(count), world, device)
     kp_total = reduce_sum(float(total_kp), world, device)
@@ -635,7 +690,7 @@ def main(argv=None):
     in_bytes = count * W * H
     alg_bytes = in_bytes + 8 * total_kp + 4 * count
     cfg_key = f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{args.nms}"
-    roofline = roofline_of(det, com, alg_bytes, in_bytes, load_traffic(cfg_key))
+    roofline = roofline_of(tm, alg_bytes, in_bytes, load_traffic(cfg_key))
 
     extras = {}
     cpu = None
@@ -647,39 +702,57 @@ def main(argv=None):
         # and without NMS", and the reference's bench times all three (benches/benchmark.rs:18-50)
         for other in [m for m in ("off", "maxt", "sad") if m != args.nms]:
             ocfg = Config(args.threshold, args.count, NonMaximalSuppression(NMS_NAMES[other]))
-            e2, d2, c2 = timed_steps(fast_hip, ctx, copies, ocfg, out, offs, stream, args.steps,
-                                     args.warmup, world, settle=args.settle_seconds)
-            e2 = reduce_max(e2, world, device)
-            kp2 = int(offs[-1].item())
-            pts2 = out[: min(kp2, cap)].cpu().numpy().astype(np.uint32)
+            t2 = timed_steps(fast_hip, lanes, bufs, copies, ocfg, args.steps, args.warmup,
+                             world, settle=args.settle_seconds)
+            e2 = reduce_max(t2.elapsed, world, device)
+            kp2 = int(bufs.offs[t2.last][-1].item())
+            pts2 = bufs.out[t2.last][: min(kp2, cap)].cpu().numpy().astype(np.uint32)
             leg = {"workload": f"same batch, nms={other}",
                    "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
                    "ms_per_step": round(e2 * 1e3 / args.steps, 4),
                    "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
-                   "roofline": roofline_of(d2, c2, in_bytes + 8 * kp2 + 4 * count, in_bytes,
+                   "roofline": roofline_of(t2, in_bytes + 8 * kp2 + 4 * count, in_bytes,
                                            load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
-                   "parity": check_parity(oracle, frames, pts2, offs.cpu().numpy(), first, count,
-                                          args.threshold, args.count, NMS_NAMES[other], W)}
+                   "parity": check_parity(oracle, frames, pts2, bufs.offs[t2.last].cpu().numpy(),
+                                          first, count, args.threshold, args.count,
+                                          NMS_NAMES[other], W)}
             extras[f"nms_{other}"] = leg
+        # the same batch on one lane (one stream: every launch waits for the previous call's
+        # compaction): the protocol of rounds 1-3, and the isolated kernel's own duration
+        lanes1 = fast_hip.Lanes(1, gpu)
+        buf1 = LaneBufs.__new__(LaneBufs)
+        buf1.out, buf1.offs = bufs.out[:1], bufs.offs[:1]
+        t1 = timed_steps(fast_hip, lanes1, buf1, copies, cfg, args.steps, args.warmup, world,
+                         settle=args.settle_seconds)
+        e1 = reduce_max(t1.elapsed, world, device)
+        kp1 = int(bufs.offs[0][-1].item())
+        extras["single_lane"] = {
+            "workload": "same batch and config, one lane (one stream)",
+            "value": round(pixels / e1 * args.steps / 1e6, 1), "unit": "Mpixels/s",
+            "ms_per_step": round(e1 * 1e3 / args.steps, 4),
+            "keypoints_equal": kp1 == total_kp,
+            "roofline": roofline_of(t1, in_bytes + 8 * kp1 + 4 * count, in_bytes,
+                                    load_traffic(cfg_key))}
     if world > 1 and not strong and not args.no_strong_leg:
         # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU (run
         # with --no-extras too: it is the multi-GPU line's own strong-scaling number)
         f4, c4 = strong_shard(rank, world, 512)
         cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29)
-        off4 = torch.zeros(c4 + 1, dtype=torch.int64, device=device)
-        e4, d4, _ = timed_steps(fast_hip, ctx, cop4, cfg, out, off4, stream, args.steps,
-                                args.warmup, world, settle=args.settle_seconds)
-        e4 = reduce_max(e4, world, device)
-        kp4 = int(reduce_sum(float(off4[-1].item()), world, device))
+        buf4 = LaneBufs(len(lanes), max(c4, 1) * 200_000, c4, device)
+        t4 = timed_steps(fast_hip, lanes, buf4, cop4, cfg, args.steps, args.warmup, world,
+                         settle=args.settle_seconds)
+        e4 = reduce_max(t4.elapsed, world, device)
+        kp4 = int(reduce_sum(float(buf4.offs[t4.last][-1].item()), world, device))
         extras["config4_strong"] = {
             "workload": f"512 {W}x{H} frames in total, {c4} per GPU (rank {rank}), "
                         f"nms={args.nms}; rotated through {len(cop4)} copies (HBM reads)",
             "value": round(512 * W * H / e4 * args.steps / 1e6, 1), "unit": "Mpixels/s",
             "ms_per_step": round(e4 * 1e3 / args.steps, 4), "scaling": "strong",
             "frames_total": 512, "keypoints_per_step": kp4,
-            "kernel_ms_avg": round(float(np.mean(d4)), 4) if len(d4) else None,
-            "kernel_ms": percentiles(d4) if len(d4) >= MIN_TIMED else None}
-        del cop4
+            "lanes": t4.lanes,
+            "kernel_ms_avg": round(t4.span_ms / t4.steps, 4),
+            "launch_ms_avg": round(float(np.mean(t4.det)), 4) if len(t4.det) else None}
+        del cop4, buf4
     if rank == 0 and not args.no_extras:
         # single-frame latency (device-resident frame, one launch, HIP events), on --input
         # when given (the reference's bench image, benches/benchmark.rs:6-16), else S1 frame 0
@@ -715,7 +788,7 @@ def main(argv=None):
             fast_hip, _native, host,
             {"off": (cfg, 0), "maxt": (cfg, 1)})
         extras["config5_4k"] = config5_4k(fast_hip, Config, NonMaximalSuppression, workloads,
-                                          out, stream, device, oracle.detect,
+                                          lanes, device, oracle.detect,
                                           settle=args.settle_seconds)
         extras["rgb_path"] = rgb_path(fast_hip, cfg, frames, out, offs, stream)
         if world == 1 and args.cpu_seconds > 0:
@@ -742,7 +815,8 @@ def main(argv=None):
                        "frames_per_gpu": count, "width": W, "height": H,
                        "threshold": args.threshold, "count": args.count, "nms": args.nms,
                        "hbm_copies": len(copies),
-                       "workspace_bytes": ctx.workspace_bytes(),
+                       "lanes": len(lanes),
+                       "workspace_bytes": sum(c.workspace_bytes() for c in lanes.ctxs),
                        "parallelism": f"frame-sharded x{world} (no collective)",
                        "ranks_share_device": bool(args.ranks_share_device)},
             "keypoints_per_step": int(kp_total),

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "fdf_pipeline_collect", "fdf_ctx_set_geometry", "fdf_ctx_timing_samples", "fdf_fetch_last",
     "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
     "fdf_detect_device_rgb", "fdf_circle", "fdf_calculate_offsets", "fdf_score_rings",
-    "fdf_score_rings_device", "fdf_ctx_set_band_rows",
+    "fdf_score_rings_device", "fdf_ctx_set_band_rows", "fdf_ctx_set_upload_chunks",
 )
 
 
@@ -163,6 +163,8 @@ def load():
     lib.fdf_ctx_set_geometry.argtypes = [vp, u32]
     lib.fdf_ctx_set_band_rows.restype = ctypes.c_int
     lib.fdf_ctx_set_band_rows.argtypes = [vp, u32]
+    lib.fdf_ctx_set_upload_chunks.restype = ctypes.c_int
+    lib.fdf_ctx_set_upload_chunks.argtypes = [vp, u32]
     lib.fdf_ctx_timing_samples.restype = ctypes.c_int
     lib.fdf_ctx_timing_samples.argtypes = [vp, vp, vp, u32, ctypes.POINTER(u32)]
     lib.fdf_fetch_last.restype = ctypes.c_int
@@ -241,6 +243,11 @@ class Context:
         """Band height override (fdf_ctx_set_band_rows): bands of ``rows`` centre rows for
         every later detection (same keypoints, other NMS tiers); 0 = automatic."""
         check(self._lib.fdf_ctx_set_band_rows(self.handle, int(rows)))
+
+    def set_upload_chunks(self, chunks=0):
+        """fdf_detect's overlapped upload (fdf_ctx_set_upload_chunks): the frame in
+        ``chunks`` row chunks while the detector runs; 1 = one copy first; 0 = default."""
+        check(self._lib.fdf_ctx_set_upload_chunks(self.handle, int(chunks)))
 
     def close(self):
         if self.handle:

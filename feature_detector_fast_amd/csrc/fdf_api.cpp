@@ -25,6 +25,7 @@
 // d_out, its offsets in d_offsets and its frames in d_in until the next host call.
 struct LastResult {
     bool valid = false;
+    bool host_out = false;         // the points / offsets are in the host-mapped h_out / h_offs
     uint64_t total = 0;
     uint32_t n_frames = 0, width = 0, height = 0;
     fdf_config cfg{};
@@ -44,6 +45,18 @@ struct fdf_ctx {
     uint8_t* d_rgb = nullptr;           size_t rgb_bytes = 0;      // host-API RGB staging
     uint2* d_out = nullptr;             size_t out_points = 0;     // host-API output
     uint64_t* d_offsets = nullptr;      size_t offsets_n = 0;      // host-API frame offsets
+    // host-API output in pinned, device-mapped host memory: the detector (direct output) or
+    // the compaction writes the points and offsets there over PCIe, so a host call needs no
+    // copy kernel, no device-to-host copy and one synchronisation (hd_*: device addresses)
+    uint2* h_out = nullptr;             uint2* hd_out = nullptr;   size_t h_out_points = 0;
+    uint64_t* h_offs = nullptr;         uint64_t* hd_offs = nullptr;   size_t h_offs_n = 0;
+    // fdf_detect's overlapped upload: the frame goes up in row chunks on copy_stream, each
+    // chunk's flag (pinned, device-mapped) set to the call's epoch after its copy, while the
+    // detector already runs and each band waits for the chunk of its last row
+    hipStream_t copy_stream = nullptr;
+    uint32_t* h_flags = nullptr;        uint32_t* hd_flags = nullptr;
+    uint32_t chunk_epoch = 0;
+    uint32_t chunks = 0;                // upload chunks (0: kChunksDefault; 1: no overlap)
     uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
@@ -101,6 +114,9 @@ struct fdf_ctx {
 constexpr size_t kMaxTimedCalls = 4096;
 constexpr uint64_t kDefaultMinTasks = 1024;   // 4 workgroups on each of 256 CUs
 constexpr uint32_t kMaxBandRows = 256;        // fdf_ctx_set_band_rows: the automatic path's range
+constexpr uint32_t kMaxChunks = 16;           // overlapped upload: chunks at most
+constexpr uint32_t kChunksDefault = 4;
+constexpr size_t kChunkMinBytes = 1u << 18;   // frames below 256 KB upload in one copy
 
 // process-wide counters: fdf_detect_batch_multi call generations, direct-output launch tags
 std::atomic<uint64_t> g_multi_gen{0};
@@ -158,6 +174,32 @@ int ensure(fdf_ctx* ctx, T** buf, size_t* have, size_t need, hipStream_t stream)
         *buf = nullptr;
         return FDF_ERR_ALLOC;
     }
+    *have = n;
+    return FDF_OK;
+}
+
+// Grow a pinned, device-mapped host buffer to `need` elements (+1/8 headroom); *dev is its
+// device address.  Like ensure(), everything the context enqueued is drained first.
+template <typename T>
+int ensure_host(fdf_ctx* ctx, T** buf, T** dev, size_t* have, size_t need, hipStream_t stream) {
+    if (*have >= need) return FDF_OK;
+    if (*buf) {
+        wait_done(ctx);
+        (void)hipStreamSynchronize(stream);
+        (void)hipHostFree(*buf);
+        *buf = *dev = nullptr;
+        *have = 0;
+    }
+    const size_t n = need + need / 8;
+    void* hp = nullptr;
+    void* dp = nullptr;
+    if (hipHostMalloc(&hp, n * sizeof(T), hipHostMallocMapped) != hipSuccess) return FDF_ERR_ALLOC;
+    if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+        (void)hipHostFree(hp);
+        return FDF_ERR_ALLOC;
+    }
+    *buf = static_cast<T*>(hp);
+    *dev = static_cast<T*>(dp);
     *have = n;
     return FDF_OK;
 }
@@ -255,12 +297,37 @@ volatile uint32_t* lookback_error_word(fdf_ctx* ctx) {
     return ctx->h_stats ? reinterpret_cast<volatile uint32_t*>(ctx->h_stats + 1) : nullptr;
 }
 
-// Takes (reads and clears) the look-back error word.
-bool take_lookback_error(fdf_ctx* ctx) {
+// Takes (reads and clears) the look-back error word: bit 0 a direct-output band's look-back
+// ran out, bit 1 a band's wait for its upload chunk.
+uint32_t take_lookback_error(fdf_ctx* ctx) {
     volatile uint32_t* e = lookback_error_word(ctx);
-    if (!e || *e == 0) return false;
+    if (!e || *e == 0) return 0;
+    const uint32_t v = *e;
     *e = 0;
-    return true;
+    return v;
+}
+
+// The overlapped upload's copy stream and chunk flags (created on first use).
+int ensure_chunk_flags(fdf_ctx* ctx) {
+    if (!ctx->copy_stream &&
+        hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+        ctx->copy_stream = nullptr;
+        return FDF_ERR_DEVICE;
+    }
+    if (!ctx->h_flags) {
+        void* hp = nullptr;
+        void* dp = nullptr;
+        if (hipHostMalloc(&hp, kMaxChunks * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+            return FDF_ERR_ALLOC;
+        if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+            (void)hipHostFree(hp);
+            return FDF_ERR_ALLOC;
+        }
+        std::memset(hp, 0, kMaxChunks * sizeof(uint32_t));
+        ctx->h_flags = static_cast<uint32_t*>(hp);
+        ctx->hd_flags = static_cast<uint32_t*>(dp);
+    }
+    return FDF_OK;
 }
 
 // Workgroups one CU holds of the detector instance for (nms, n) with `lds` bytes of LDS, from
@@ -275,9 +342,15 @@ uint32_t wg_per_cu(fdf_ctx* ctx, uint32_t nms, uint32_t n, uint32_t lds, bool rg
     return (uint32_t)wg;
 }
 
+struct ChunkedUpload {
+    const uint32_t* flags = nullptr;   // device address of the chunk flags (NULL: none)
+    uint32_t rows = 0, epoch = 0;
+};
+
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
-            uint64_t* d_offsets, hipStream_t stream, bool rgb = false) {
+            uint64_t* d_offsets, hipStream_t stream, bool rgb = false,
+            const ChunkedUpload& up = ChunkedUpload{}) {
     double density = 0.0;
     if (!ctx->h_stats) {
         void* hp = nullptr;
@@ -426,6 +499,9 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.ticket = ctx->d_sums + 2 * fdfk::kMaxGroupSums + 2;
     p.ticket_base = ctx->ticket_next;
     p.lookback_error = ctx->h_stats ? reinterpret_cast<uint32_t*>(ctx->d_stats + 1) : nullptr;
+    p.chunk_flags = up.flags;
+    p.chunk_rows = up.rows;
+    p.chunk_epoch = up.epoch;
     if (direct) {
         // a (re)allocated buffer is zeroed: recycled device memory can hold descriptors of
         // another context's launches.  Launch tags are unique in the process as well.
@@ -526,14 +602,17 @@ int check_host_args(const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t
 
 // Phase 1 of a host detection (lock held): frames in, detection + compaction into the
 // context's output buffer, frame offsets back to the host (`offs`, n_frames + 1 entries).
-// The device output starts small and grows to the keypoint total; when it has to grow only
-// the compaction is run again (the per-band slots still hold the detection).  On success
-// ctx->last describes the result, which stays on the device until the next host call.
+// The output starts small and grows to the keypoint total; when it has to grow only the
+// compaction is run again (the per-band slots still hold the detection).  On success
+// ctx->last describes the result, which stays in the context until the next host call.
+// `host_out`: the output is the pinned, device-mapped h_out / h_offs (the kernels write the
+// points and offsets into host memory: no copy back, one synchronisation); otherwise the
+// device buffers d_out / d_offsets (the scored calls, whose score kernel reads the points).
 // `rgb`: the frames are RGB8 (rows of 3 * w bytes at row_stride), converted on the device
 // with image 0.24.6's to_luma8 before detection (src/main.rs:58).
 int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
              size_t row_stride, size_t frame_stride, const fdf_config* cfg, bool rgb,
-             uint64_t* offs) {
+             uint64_t* offs, bool host_out) {
     ctx->last = LastResult{};          // invalid, and not a shard of a multi-context call
     const size_t frame_bytes = (size_t)w * h;
     const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
@@ -541,8 +620,26 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     const size_t guess = std::min(max_points, std::max<size_t>(4096, frame_bytes / 64 * n_frames));
     int rc;
     if ((rc = ensure(ctx, &ctx->d_in, &ctx->in_bytes, frame_bytes * n_frames, ctx->stream))) return rc;
-    if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, guess, ctx->stream))) return rc;
-    if ((rc = ensure(ctx, &ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, ctx->stream))) return rc;
+    uint2* out_dev;                    // the output as the kernels address it
+    uint64_t* offs_dev;
+    size_t* out_cap;
+    if (host_out) {
+        if ((rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points, guess, ctx->stream)))
+            return rc;
+        if ((rc = ensure_host(ctx, &ctx->h_offs, &ctx->hd_offs, &ctx->h_offs_n, n_frames + 1ull,
+                              ctx->stream)))
+            return rc;
+        out_dev = ctx->hd_out;
+        offs_dev = ctx->hd_offs;
+        out_cap = &ctx->h_out_points;
+    } else {
+        if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, guess, ctx->stream))) return rc;
+        if ((rc = ensure(ctx, &ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, ctx->stream)))
+            return rc;
+        out_dev = ctx->d_out;
+        offs_dev = ctx->d_offsets;
+        out_cap = &ctx->out_points;
+    }
     const size_t px = rgb ? 3 : 1;                 // bytes per pixel of the host frames
     uint8_t* stage = ctx->d_in;
     if (rgb) {
@@ -550,17 +647,53 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             return rc;
         stage = ctx->d_rgb;
     }
-    // the host frames are read by the copies below: nothing else may still read d_in
+    // the host frames are read by the copies below: nothing else may still read d_in (nor
+    // the host output, which the host reads after this call)
     wait_done(ctx);
-    for (uint32_t f = 0; f < n_frames; ++f) {
-        const uint8_t* src = data + (size_t)f * frame_stride;
-        uint8_t* dst = stage + (size_t)f * frame_bytes * px;
-        hipError_t e = row_stride == px * w
-                           ? hipMemcpyAsync(dst, src, frame_bytes * px, hipMemcpyHostToDevice,
-                                            ctx->stream)
-                           : hipMemcpy2DAsync(dst, px * w, src, row_stride, px * w, h,
-                                              hipMemcpyHostToDevice, ctx->stream);
-        if (e != hipSuccess) return FDF_ERR_DEVICE;
+    // one grey frame of >= kChunkMinBytes: upload it in row chunks on the copy stream while
+    // the detector runs, each band waiting for the chunk of its last row (the H2D of a 1080p
+    // frame is ~45 us, the detector ~20 us: DESIGN.md §7.5)
+    ChunkedUpload up;
+#ifdef FDF_DEBUG_BUILD   // A/B of the overlapped upload (tools/host_latency.py): FDF_CHUNKS=1 disables it
+    if (const char* e = std::getenv("FDF_CHUNKS")) ctx->chunks = (uint32_t)std::strtoul(e, nullptr, 0);
+#endif
+    const bool chunked = host_out && !rgb && n_frames == 1 && frame_bytes >= kChunkMinBytes &&
+                         ctx->chunks != 1 && ctx->h_stats && ensure_chunk_flags(ctx) == FDF_OK;
+    if (chunked) {
+        const uint32_t nchunks = std::min<uint32_t>(ctx->chunks ? ctx->chunks : kChunksDefault,
+                                                    kMaxChunks);
+        up.rows = (h + nchunks - 1) / nchunks;
+        up.epoch = ++ctx->chunk_epoch == 0 ? ++ctx->chunk_epoch : ctx->chunk_epoch;
+        up.flags = ctx->hd_flags;
+        for (uint32_t r0 = 0, c = 0; r0 < h; r0 += up.rows, ++c) {
+            const uint32_t nr = std::min(up.rows, h - r0);
+            const uint8_t* src = data + (size_t)r0 * row_stride;
+            uint8_t* dst = ctx->d_in + (size_t)r0 * w;
+            hipError_t e = row_stride == w
+                               ? hipMemcpyAsync(dst, src, (size_t)nr * w, hipMemcpyHostToDevice,
+                                                ctx->copy_stream)
+                               : hipMemcpy2DAsync(dst, w, src, row_stride, w, nr,
+                                                  hipMemcpyHostToDevice, ctx->copy_stream);
+            if (e == hipSuccess) e = hipStreamWriteValue32(ctx->copy_stream, ctx->hd_flags + c, up.epoch, 0);
+            if (e != hipSuccess) {
+                // the runtime cannot do this upload: one copy before the launch, from now on
+                (void)hipStreamSynchronize(ctx->copy_stream);
+                ctx->chunks = 1;
+                return run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb,
+                                offs, host_out);
+            }
+        }
+    } else {
+        for (uint32_t f = 0; f < n_frames; ++f) {
+            const uint8_t* src = data + (size_t)f * frame_stride;
+            uint8_t* dst = stage + (size_t)f * frame_bytes * px;
+            hipError_t e = row_stride == px * w
+                               ? hipMemcpyAsync(dst, src, frame_bytes * px, hipMemcpyHostToDevice,
+                                                ctx->stream)
+                               : hipMemcpy2DAsync(dst, px * w, src, row_stride, px * w, h,
+                                                  hipMemcpyHostToDevice, ctx->stream);
+            if (e != hipSuccess) return FDF_ERR_DEVICE;
+        }
     }
     // RGB: a luma pass, then the grey detector.  The detector with luma converted in its
     // loads (fdf_detect_device_rgb) is correct but measured 1.6x slower on 256 1080p frames:
@@ -569,41 +702,71 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
-    rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, ctx->d_out, ctx->out_points,
-                 ctx->d_offsets, ctx->stream);
+    rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, out_dev, *out_cap, offs_dev,
+                 ctx->stream, false, up);
+    if (chunked) {
+        // the copies end before the detector does (it waits for the last one), but a failed
+        // launch or a timed-out wait would leave them running: drain them before any return
+        const hipError_t e = hipStreamSynchronize(ctx->copy_stream);
+        if (!rc && e != hipSuccess) rc = FDF_ERR_DEVICE;
+    }
     if (rc) return rc;
-    hipError_t e = hipMemcpyAsync(offs, ctx->d_offsets, sizeof(uint64_t) * (n_frames + 1ull),
-                                  hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) return FDF_ERR_DEVICE;
-    if (take_lookback_error(ctx)) {
+    // the offsets on the host: read in place (host output) or copied back
+    auto fetch_offsets = [&]() -> hipError_t {
+        hipError_t e = hipSuccess;
+        if (!host_out)
+            e = hipMemcpyAsync(offs, offs_dev, sizeof(uint64_t) * (n_frames + 1ull),
+                               hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess && host_out)
+            std::memcpy(offs, ctx->h_offs, sizeof(uint64_t) * (n_frames + 1ull));
+        return e;
+    };
+    if (fetch_offsets() != hipSuccess) return FDF_ERR_DEVICE;
+    if (const uint32_t err = take_lookback_error(ctx)) {
+        if (err & 2u) {
+            // a band's wait for its upload chunk ran out (the copies are drained now): detect
+            // again from the whole frame, uploaded before the launch
+            const uint32_t saved = ctx->chunks;
+            ctx->chunks = 1;
+            rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs,
+                          host_out);
+            ctx->chunks = saved;
+            return rc;
+        }
         // a direct-output band's look-back ran out (band_lookback): the offsets and points of
         // its frame on are not written; the slots and counts are, so the compaction rebuilds
         // both from them
         fdfk::CompactParams c = ctx->last_compact;
         c.kp_stats = nullptr;
         c.group_sums = nullptr;
-        e = fdfk::launch_compact(c, ctx->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(offs, ctx->d_offsets, sizeof(uint64_t) * (n_frames + 1ull),
-                               hipMemcpyDeviceToHost, ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e != hipSuccess) return FDF_ERR_DEVICE;
+        if (fdfk::launch_compact(c, ctx->stream) != hipSuccess || fetch_offsets() != hipSuccess)
+            return FDF_ERR_DEVICE;
     }
     const uint64_t total = offs[n_frames];
-    if (total > ctx->out_points) {
+    if (total > *out_cap) {
         // grow the output and compact again (the offsets do not change)
         fdfk::CompactParams c = ctx->last_compact;
-        if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (size_t)total, ctx->stream))) return rc;
-        c.out = ctx->d_out;
-        c.cap = ctx->out_points;
+        if (host_out) {
+            if ((rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points, (size_t)total,
+                                  ctx->stream)))
+                return rc;
+            c.out = ctx->hd_out;
+        } else {
+            if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (size_t)total, ctx->stream))) return rc;
+            c.out = ctx->d_out;
+        }
+        c.cap = *out_cap;
         c.kp_stats = nullptr;           // already reported (and reset) by the first compaction
         if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
             hipEventRecord(ctx->done, ctx->stream) != hipSuccess)
             return FDF_ERR_DEVICE;
         ctx->done_stream = ctx->stream;
+        // the host reads h_out next: the compaction must be done
+        if (host_out && hipStreamSynchronize(ctx->stream) != hipSuccess) return FDF_ERR_DEVICE;
     }
     ctx->last.valid = true;
+    ctx->last.host_out = host_out;
     ctx->last.total = total;
     ctx->last.n_frames = n_frames;
     ctx->last.width = w;
@@ -629,13 +792,21 @@ int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
                                          ctx->stream) != hipSuccess)
                 return FDF_ERR_DEVICE;
         }
+        // (a host-output result's points and offsets are read through their device-mapped
+        // addresses)
         e = fdfk::launch_score_frames(ctx->d_in, L.width, (uint64_t)L.width * L.height,
-                                      L.n_frames, ctx->d_out, ctx->d_offsets, n,
+                                      L.n_frames, L.host_out ? ctx->hd_out : ctx->d_out,
+                                      L.host_out ? ctx->hd_offs : ctx->d_offsets, n,
                                       score_blocks(n, L.n_frames), score_kind(L.cfg.nms),
                                       L.cfg.threshold, L.cfg.count, ctx->d_scores, ctx->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(out_scores, ctx->d_scores, n * sizeof(uint16_t),
                                hipMemcpyDeviceToHost, ctx->stream);
+    }
+    if (L.host_out) {
+        if (e == hipSuccess && out_scores) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) std::memcpy(out, ctx->h_out, n * sizeof(fdf_point));
+        return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(out, ctx->d_out, n * sizeof(fdf_point), hipMemcpyDeviceToHost,
@@ -671,7 +842,9 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
         local.resize(n_frames + 1ull);
         offs = local.data();
     }
-    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs);
+    // unscored calls take the host-mapped output (no copy back); the scored ones keep the
+    // points on the device for the score kernel
+    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored);
     if (rc) return rc;
     const uint64_t total = offs[n_frames];
     rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
@@ -767,6 +940,10 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         (void)hipFree(ctx->d_rgb);
         (void)hipFree(ctx->d_out);
         (void)hipFree(ctx->d_offsets);
+        if (ctx->h_out) (void)hipHostFree(ctx->h_out);
+        if (ctx->h_offs) (void)hipHostFree(ctx->h_offs);
+        if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+        if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
         (void)hipFree(ctx->d_scores);
         (void)hipFree(ctx->d_slots);
         (void)hipFree(ctx->d_counts);
@@ -806,6 +983,13 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
     if (!ctx) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->min_tasks = min_tasks;
+    return FDF_OK;
+}
+
+int fdf_ctx_set_upload_chunks(fdf_ctx* ctx, uint32_t chunks) {
+    if (!ctx || chunks > kMaxChunks) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->chunks = chunks;
     return FDF_OK;
 }
 
@@ -1172,7 +1356,7 @@ int fdf_detect_batch_multi(fdf_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* 
         DeviceGuard guard(ctx->device);
         local[k].assign(nf + 1ull, 0);
         status[k] = run_host(ctx, data + (size_t)first[k] * frame_stride_bytes, nf, width, height,
-                             width, frame_stride_bytes, cfg, false, local[k].data());
+                             width, frame_stride_bytes, cfg, false, local[k].data(), true);
     };
     auto run_all = [&](auto&& fn) {
         std::vector<std::thread> pool;

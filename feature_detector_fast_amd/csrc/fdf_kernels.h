@@ -206,6 +206,14 @@ struct BandParams {
     // Direct output: set when a look-back wait ran out (host-mapped; the band then publishes
     // no prefix and writes no points, and the host recovers from the slots: fdf_api.cpp)
     uint32_t* lookback_error;
+    // Host frames arriving in row chunks while the kernel runs (fdf_detect's overlapped
+    // upload; NULL: the frames are in place): chunk c = rows [c * chunk_rows, (c+1) *
+    // chunk_rows) has landed once chunk_flags[c] == chunk_epoch (host-mapped words the copy
+    // stream writes after each chunk's copy, in order).  A band waits for the chunk of the
+    // last row it reads before its first load; a wait that runs out sets lookback_error.
+    const uint32_t* chunk_flags;
+    uint32_t chunk_rows;
+    uint32_t chunk_epoch;
 };
 constexpr uint64_t kLbAggregate = 1ull << 30;   // value = the band's own keypoint count
 constexpr uint64_t kLbPrefix = 1ull << 31;      // value = keypoints of bands 0 .. this one

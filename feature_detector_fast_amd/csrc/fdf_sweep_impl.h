@@ -1186,6 +1186,24 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         }
         reinterpret_cast<uint32_t*>(smem_raw + L.seltab)[tid] = word;
     }
+    if (P.chunk_flags && tid == 0) {
+        // an overlapped upload (fdf_detect): wait for the chunk holding the last row the band
+        // reads -- its tested rows (with the NMS halo row) + 3 -- then acquire at system
+        // scope, so that no line of the frame cached before the copy landed is read
+        const uint32_t last_row = min(H - 1, y0 + rows + halo + 2);
+        uint32_t* flag = const_cast<uint32_t*>(P.chunk_flags) + last_row / P.chunk_rows;
+        uint32_t polls = 0;
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != P.chunk_epoch) {
+            if (++polls > (1u << 20)) {               // ~30 ms: the copy never landed
+                if (P.lookback_error)
+                    __hip_atomic_fetch_or(P.lookback_error, 2u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
     __syncthreads();
     if constexpr (kDebugBuild) ph[0] = __builtin_amdgcn_s_memtime();   // setup done
 

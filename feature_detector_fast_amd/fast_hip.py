@@ -234,13 +234,14 @@ def detector_batch(frames, config, device=0, devices=None):
     return out[: n.value], offsets
 
 
-def detect_device(frames, config, out, offsets, stream=None, device=None):
+def detect_device(frames, config, out, offsets, stream=None, device=None, ctx=None):
     """Enqueue detection on device-resident frames; nothing crosses PCIe.
 
     ``frames``: torch uint8 CUDA tensor (F, H, W), contiguous.  ``out``: int32/uint32 CUDA
     tensor (cap, 2).  ``offsets``: int64 CUDA tensor (F+1,).  Asynchronous on ``stream``
     (a torch.cuda.Stream; default: torch's current stream).  On completion
-    offsets[F] holds the total (even when it exceeds ``cap``)."""
+    offsets[F] holds the total (even when it exceeds ``cap``).  ``ctx``: the context whose
+    workspace the call uses (default: the device's process-wide one; see :class:`Lanes`)."""
     import torch
 
     if frames.dim() != 3 or frames.dtype != torch.uint8 or not frames.is_contiguous():
@@ -253,7 +254,8 @@ def detect_device(frames, config, out, offsets, stream=None, device=None):
         raise ValueError("out must be a contiguous (cap, 2) 32-bit tensor")
     dev = frames.device.index if device is None else device
     cfg = _to_c_config(config)
-    ctx = context(dev)
+    if ctx is None:
+        ctx = context(dev)
     if stream is None:
         stream = torch.cuda.current_stream(frames.device)
     f, h, w = frames.shape
@@ -261,6 +263,68 @@ def detect_device(frames, config, out, offsets, stream=None, device=None):
         ctx.handle, frames.data_ptr(), f, w, h, h * w, ctypes.byref(cfg), out.data_ptr(),
         out.shape[0], offsets.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
     check(rc, "fdf_detect_device")
+
+
+class Lanes:
+    """``n`` launch lanes on one device for back-to-back device-resident batches: lane i is a
+    context of its own (workspace: band slots, counts, sums) and the HIP stream that context
+    created.  Call k goes to lane k % n with no dependency on the other lanes, so one call's
+    detector runs beside the previous calls' last workgroups and compaction: with n = 3, 512
+    1080p frames take 0.391 ms per call against 0.442 ms on one stream.
+
+    Ordering: with ``after_current=True`` (default) each call first makes its lane wait for
+    the work already enqueued on torch's current stream (the producer of ``frames``), and
+    :meth:`wait` makes the current stream wait for a lane's last call (before reading its
+    ``out`` / ``offsets``).  Each lane needs its own ``out`` / ``offsets`` buffers while its
+    call may still run."""
+
+    def __init__(self, n=3, device=0):
+        if n < 1:
+            raise ValueError("at least one lane")
+        self.device = int(device)
+        self.ctxs = [context(self.device)]
+        for _ in range(n - 1):
+            ctx = _native.Context(self.device)
+            ctx.lock = threading.Lock()
+            self.ctxs.append(ctx)
+        self._ext = [None] * n
+
+    def __len__(self):
+        return len(self.ctxs)
+
+    def stream(self, lane):
+        """Lane ``lane``'s HIP stream as a torch.cuda.ExternalStream (events, waits)."""
+        import torch
+
+        if self._ext[lane] is None:
+            self._ext[lane] = torch.cuda.ExternalStream(self.ctxs[lane].stream,
+                                                        device=torch.device("cuda", self.device))
+        return self._ext[lane]
+
+    def detect_device(self, k, frames, config, out, offsets, after_current=True):
+        """detect_device on lane k % n (asynchronous on that lane's stream)."""
+        import torch
+
+        lane = k % len(self.ctxs)
+        s = self.stream(lane)
+        if after_current:
+            s.wait_stream(torch.cuda.current_stream(frames.device))
+        detect_device(frames, config, out, offsets, stream=s, device=self.device,
+                      ctx=self.ctxs[lane])
+        return lane
+
+    def wait(self, lane=None):
+        """Make torch's current stream wait for lane ``lane`` (every lane when None)."""
+        import torch
+
+        cur = torch.cuda.current_stream(torch.device("cuda", self.device))
+        for i in (range(len(self.ctxs)) if lane is None else [lane]):
+            cur.wait_stream(self.stream(i))
+
+    def close(self):
+        for ctx in self.ctxs[1:]:
+            ctx.close()
+        self.ctxs = self.ctxs[:1]
 
 
 def detect_device_rgb(frames, config, out, offsets, stream=None, device=None):
@@ -446,7 +510,7 @@ def score_device(frames, config, points, offsets, scores, stream=None, device=No
 
 
 __all__ = ["NORTH", "EAST", "SOUTH", "WEST", "circle", "calculate_offsets", "context",
-           "shard_contexts", "capacity_guess",
+           "shard_contexts", "capacity_guess", "Lanes",
            "detect_array", "detector", "detector_batch", "detect_device", "keypoint_scores",
            "detect_scored_array", "detector_scored", "detector_batch_scored", "score_device",
            "detect_rgb_array", "detector_rgb", "rgb_to_luma", "detect_device_rgb",

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FDF_ABI_VERSION 4
+#define FDF_ABI_VERSION 5
 
 /* Status codes.  Shapes the reference maps to an empty Vec return FDF_OK with 0 points. */
 enum fdf_status {
@@ -115,6 +115,13 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
  * tests use it to cross the band NMS pass's LDS / spill / dense tiers.  rows > 256 (outside
  * the automatic choice's range): FDF_ERR_ARG. */
 int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows);
+
+/* Overlapped upload (extension): fdf_detect uploads a frame of >= 256 KB in `chunks` row
+ * chunks (default 0 = 4, at most 16) on a copy stream of the context while the detector
+ * already runs; each band waits (on the device) for the chunk holding the last row it reads,
+ * so the upload overlaps the detection.  chunks = 1: one copy before the launch.  The
+ * keypoints are the same either way. */
+int fdf_ctx_set_upload_chunks(fdf_ctx* ctx, uint32_t chunks);
 
 /* Device bytes the context's workspace holds now (host-API staging and output, per-band
  * slots and counts, compaction sums).  Slots take 1/8 byte per pixel of the largest batch

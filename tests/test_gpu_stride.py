@@ -207,3 +207,30 @@ def test_concurrent_direct_grids_device():
             assert np.array_equal(o, o0) and np.array_equal(p, p0)
         for f in (0, 7):
             assert np.array_equal(p0[o0[f]:o0[f + 1]], oracle.detect(hosts[k][f], 16, 9, 1)), (k, f)
+
+
+@pytest.mark.parametrize("chunks", [0, 2, 16, 1])
+def test_host_overlapped_upload(chunks):
+    """fdf_detect's overlapped upload (fdf_ctx_set_upload_chunks): the frame goes up in row
+    chunks while the detector runs, each band waiting for the chunk of its last row.  Frames
+    alternate between contents (a band reading a row before its chunk landed, or a stale
+    cached line of the previous frame, would show as a wrong list), with packed and padded
+    row strides; every list equals the oracle.  chunks = 1 is the one-copy path."""
+    ctx = fast_hip.context(0)
+    frames = [workloads.s1_frame(31), workloads.s3_frame(12), workloads.s2_frame(9),
+              workloads.s1_frame(77)]
+    want = {(i, nms): oracle.detect(f, 16, 9, nms) for i, f in enumerate(frames) for nms in (0, 1)}
+    ctx.set_upload_chunks(chunks)
+    try:
+        for rep in range(2):
+            for i, f in enumerate(frames):
+                nms = (i + rep) % 2
+                img = f
+                if (i + rep) % 3 == 2:          # a padded row stride (hipMemcpy2DAsync chunks)
+                    padded = np.full((f.shape[0], f.shape[1] + 40), 0xFF, dtype=np.uint8)
+                    padded[:, : f.shape[1]] = f
+                    img = padded[:, : f.shape[1]]
+                got = fast_hip.detect_array(img, Config(16, 9, NonMaximalSuppression(nms)))
+                assert np.array_equal(got, want[(i, nms)]), (rep, i, nms)
+    finally:
+        ctx.set_upload_chunks(0)

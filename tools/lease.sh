@@ -17,6 +17,7 @@
 #   single|NAME                        single-frame latency + kernel traces (off, max-t)
 #   py|NAME|SCRIPT ARGS                python3 SCRIPT ARGS             -> NAME.json
 #   trace|NAME|SCRIPT ARGS[|LAST]      rocprofv3 kernel trace of a script -> NAME.json (overlap, gaps)
+#   htrace|NAME|SCRIPT ARGS            kernel + memory-copy trace of a host-API script -> NAME.json
 set -o pipefail
 O=gpurun_out/${1:?out}; shift
 mkdir -p "$O"
@@ -113,6 +114,11 @@ for STEP in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/$A1" -o p -- python3 $A2 > "$O/$A1.out" 2> "$L" || fail "$STEP" "$L"
       python3 tools/trace_overlap.py "$O/$A1" --last ${A3:-200} > "$O/$A1.json" || fail "$STEP overlap" "$O/$A1.json"
       cat "$O/$A1.json"; rm -rf "$O/$A1" ;;
+    htrace)
+      # kernel + memory-copy trace of a host-API script, cut into calls (tools/host_timeline.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/$A1" -o p -- python3 $A2 > "$O/$A1.out" 2> "$L" || fail "$STEP" "$L"
+      python3 tools/host_timeline.py "$O/$A1" > "$O/$A1.json" || fail "$STEP timeline" "$O/$A1.json"
+      cat "$O/$A1.out" "$O/$A1.json"; rm -rf "$O/$A1" ;;
     *)
       echo "unknown step kind: $KIND"; exit 2 ;;
   esac
