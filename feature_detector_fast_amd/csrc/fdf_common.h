@@ -35,6 +35,22 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
+// base + the set bits of `mask` below this lane (mbcnt's accumulator: no separate add)
+__device__ __forceinline__ uint32_t lanes_below_plus(uint64_t mask, uint32_t base) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, base));
+}
+// sel ? a : b, bit by bit, in one v_bitop3 (LUT 0xCA: src0 selects src1 over src2)
+__device__ __forceinline__ uint32_t bitop3_sel(uint32_t sel, uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_bitop3_b32(sel, a, b, 0xCA);
+}
+// a * b for a, b < 2^24 as one full-rate v_mul_u32_u24 (the compiler turns both the
+// masked product and __umul24 into a quarter-rate v_mul_lo_u32 here); `a` wave-uniform
+__device__ __forceinline__ uint32_t mul_u24_s(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(a), "v"(b));
+    return r;
+}
 
 // Division by a per-launch divisor d (a frame width, bitmap words per row) for x < 2^24:
 // q = hi32(x * m) with m = ceil(2^32 / d) is q_true or q_true + 1 (x * (m d - 2^32) / d

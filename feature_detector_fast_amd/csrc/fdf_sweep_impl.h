@@ -456,9 +456,8 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
             if (is_kp) sh.stage[(q + lanes_below(bal)) & 63u] = u.lane;
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // see issue_batch
             const int src = (int)(sh.stage[u.lane] << 2);
-            // list position (bitmap row * W + x): masked operands make it a full-rate
-            // v_mul_u32_u24 (__umul24 here compiled to a quarter-rate v_mul_lo_u32)
-            const uint32_t pk = ((((uint32_t)(y - u.yb) & 0x3ffu) * (u.src.W & 0xffffffu) + (uint32_t)x) << 12) |
+            // list position (bitmap row * W + x) with a full-rate 24-bit multiply
+            const uint32_t pk = ((mul_u24_s(u.src.W, (uint32_t)(y - u.yb) & 0x3ffu) + (uint32_t)x) << 12) |
                                 (kd ? 0x100u : 0u) | c;
             uint32_t nwv[4];
 #pragma unroll
@@ -492,7 +491,7 @@ __device__ __forceinline__ void evaluate_batch(const SweepShared& sh, UnitCtx& u
             if (is_kp) {
                 const uint32_t score = score_sum_abs_packed(c, w, u.t);
                 const uint32_t idx = base + lanes_below(bal);
-                const uint32_t e = ((((uint32_t)(y - u.yb) & 0x3ffu) * (u.src.W & 0xffffffu) + (uint32_t)x) << 12) | score;
+                const uint32_t e = ((mul_u24_s(u.src.W, (uint32_t)(y - u.yb) & 0x3ffu) + (uint32_t)x) << 12) | score;
                 if (idx < sh.slist_cap) sh.slist[idx] = e;
                 else if (idx - sh.slist_cap < sh.spill_cap) sh.spill[idx - sh.slist_cap] = e;
             }
@@ -664,17 +663,16 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         /* lane is bit 8j + 4 + m (bit 7 of byte j of cand[m], moved by bit-field */         \
         /* inserts), the row and lane code in the low nibbles */                             \
         static_assert(M == 4, "four flag dwords per lane row");                              \
-        uint32_t cm = cand[3];                           \
-        cm = (cm & 0x80808080u) | ((cand[2] >> 1) & ~0x80808080u);                           \
-        cm = (cm & 0xC0C0C0C0u) | ((cand[1] >> 2) & ~0xC0C0C0C0u);                           \
-        cm = (cm & 0xE0E0E0E0u) | ((cand[0] >> 3) & ~0xE0E0E0E0u);                           \
-        cm &= vmask;                                                                         \
+        /* three select-by-mask bitop3s (each after a shift), then the column mask */       \
+        uint32_t cm = bitop3_sel(0x80808080u, cand[3], cand[2] >> 1);                        \
+        cm = bitop3_sel(0xC0C0C0C0u, cm, cand[1] >> 2);                                      \
+        cm = bitop3_sel(0xE0E0E0E0u, cm, cand[0] >> 3) & vmask;                              \
         if (live) {                                                                          \
             const bool has = cm != 0u;                                                       \
             const uint64_t bal = wave_ballot(has);                                           \
             if (has)                                                                         \
                 sh.pq[(u.tail + lanes_below(bal)) & (kSweepPixelQ - 1)] =                    \
-                    cm | lane_code | row_code | spread_code((uint32_t)(J) << 6);             \
+                    cm | lane_row_code | spread_code((uint32_t)(J) << 6);                    \
             u.tail += (uint32_t)__popcll(bal);                                               \
             while (u.tail - u.head > kSweepPixelQ - 64) {                                    \
                 /* dense image: test the oldest pixels now, synchronously */                 \
@@ -700,7 +698,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                   "issue points per loop body must cycle through the batch slots");
     for (int i0 = 0; i0 < T; i0 += K) {
         // FIFO code of row ys + i0 + J: i0 is a multiple of K, so its spread ORs with J's
-        const uint32_t row_code = spread_code((uint32_t)i0 << 6);
+        const uint32_t lane_row_code = lane_code | spread_code((uint32_t)i0 << 6);
         FDF_SWEEP_STEP(0)
         FDF_SWEEP_STEP(1)
         FDF_SWEEP_STEP(2)
@@ -1186,16 +1184,19 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         }
         reinterpret_cast<uint32_t*>(smem_raw + L.seltab)[tid] = word;
     }
-    if (P.chunk_flags && tid == 0) {
-        // an overlapped upload (fdf_detect): wait for the chunk holding the last row the band
-        // reads -- its tested rows (with the NMS halo row) + 3 -- then acquire at system
-        // scope, so that no line of the frame cached before the copy landed is read
+    if (P.chunk_flags && wave == 0) {
+        // an overlapped upload (fdf_detect): wave 0 waits for the chunk holding the last row
+        // the band reads -- its tested rows (with the NMS halo row) + 3 -- then acquires at
+        // system scope, so that no line of the frame cached before the copy landed is read.
+        // (Wave-uniform control flow: a per-thread wait loop costs the sweep registers.)
         const uint32_t last_row = min(H - 1, y0 + rows + halo + 2);
         uint32_t* flag = const_cast<uint32_t*>(P.chunk_flags) + last_row / P.chunk_rows;
-        uint32_t polls = 0;
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != P.chunk_epoch) {
-            if (++polls > (1u << 20)) {               // ~30 ms: the copy never landed
-                if (P.lookback_error)
+        for (uint32_t polls = 0;; ++polls) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+            if (v == P.chunk_epoch) break;
+            if (polls > (1u << 20)) {                 // ~30 ms: the copy never landed
+                if (P.lookback_error && lane == 0)
                     __hip_atomic_fetch_or(P.lookback_error, 2u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
@@ -1449,6 +1450,9 @@ typedef void (*SweepKernelFn)(BandParams);
 
 template <int NMS>
 static SweepKernelFn pick_sweep_n(uint32_t n) {
+#ifdef FDF_ISA_ONE_N   // ISA studies only (tools/isa_loops.py): one count per NMS mode, fast to compile
+    return n == FDF_ISA_ONE_N ? fast_sweep_kernel<NMS, FDF_ISA_ONE_N> : nullptr;
+#endif
     switch (n) {
         case 9: return fast_sweep_kernel<NMS, 9>;
         case 10: return fast_sweep_kernel<NMS, 10>;

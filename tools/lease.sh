@@ -12,6 +12,7 @@
 #   pmc|NAME|VARIANT|ARGS              SQ / TCC counter passes of one variant (debug build)
 #   pmcv|NAME|VARIANTS|ARGS            one instruction-count pass per variant (debug build)
 #   pmct|NAME|VARIANTS|ARGS            L2 hit/miss + FETCH_SIZE (+ VALU/VMEM) per variant (debug build)
+#   pmcx|NAME|VARIANTS|ARGS|COUNTERS   one pass of the given counters per variant (debug build)
 #   stamps|NAME|ARGS                   tools/stamps.py ARGS (debug build) -> NAME.json
 #   profile|TAG|ARGS                   tools/profile_round.sh TAG ARGS (kernel stats + traffic)
 #   single|NAME                        single-frame latency + kernel traces (off, max-t)
@@ -91,6 +92,18 @@ for STEP in "$@"; do
               python3 tools/ablate.py --rounds 1 --iters 2 $A3 --variants "$v" > "$D/${t}_$k.log" 2>&1 || fail "$STEP $v $k" "$D/${t}_$k.log"
         done
         echo "$v $(python3 tools/pmc_summary.py "$D/${t}_1" "$D/${t}_2" "$D/${t}_3" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(json.dumps({k: round(v) for k, v in d.items() if not k.startswith("_")}))')" >> "$O/$A1.txt"
+      done
+      cat "$O/$A1.txt"
+      rm -rf "$D" ;;
+    pmcx)
+      # one pass of the given counters (A4, space-separated, one block's limits) per variant
+      D="$O/$A1"; mkdir -p "$D"; : > "$O/$A1.txt"
+      IFS=',' read -r -a VS <<< "$A2"
+      for v in "${VS[@]}"; do
+        t=$(echo "$v" | tr ':.' '__')
+        FDF_LIB_PATH=$DEBUG_LIB timeout -s KILL 120 rocprofv3 --pmc $A4 -d "$D/$t" -o p --output-format csv -- \
+            python3 tools/ablate.py --rounds 1 --iters 2 $A3 --variants "$v" > "$D/$t.log" 2>&1 || fail "$STEP $v" "$D/$t.log"
+        echo "$v $(python3 tools/pmc_summary.py "$D/$t" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(json.dumps({k: round(v) for k, v in d.items() if not k.startswith("_")}))')" >> "$O/$A1.txt"
       done
       cat "$O/$A1.txt"
       rm -rf "$D" ;;

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--lanes", default="1,2", help="comma-separated lane counts to time")
     ap.add_argument("--torch-streams", action="store_true", help="also time 2 lanes on torch streams")
     ap.add_argument("--settle", type=float, default=1.0)
+    ap.add_argument("--rows", default="0",
+                    help="band heights to time (fdf_ctx_set_band_rows on every lane; 0 = automatic)")
     args = ap.parse_args()
     import ctypes
 
@@ -60,9 +62,21 @@ def main():
                                    offs[i].data_ptr(), ctypes.c_void_p(stream))
         _native.check(rc, "fdf_detect_device")
 
-    shapes = {f"lanes{n}": (lambda n: lambda k: call(k, k % n, ctxs[k % n].stream))(n) for n in lanes}
-    if args.torch_streams:
-        shapes["torch2"] = lambda k: call(k, k & 1, tstreams[k & 1])
+    def with_rows(r, fn):
+        def run(k):
+            if k == 0:
+                for c in ctxs:
+                    c.set_band_rows(r)
+            fn(k)
+        return run
+
+    shapes = {}
+    for r in [int(x) for x in args.rows.split(",")]:
+        tag = "" if r == 0 else f"_rows{r}"
+        for n in lanes:
+            shapes[f"lanes{n}{tag}"] = with_rows(r, (lambda n: lambda k: call(k, k % n, ctxs[k % n].stream))(n))
+        if args.torch_streams:
+            shapes[f"torch2{tag}"] = with_rows(r, lambda k: call(k, k & 1, tstreams[k & 1]))
     t_end = time.perf_counter() + args.settle
     while time.perf_counter() < t_end:
         for k in range(20):
