@@ -73,6 +73,7 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
 
 struct RowSource {
     __amdgpu_buffer_rsrc_t rs;   // the frame; num_records = W * H + 15, or W * H when EXACT
+    __amdgpu_buffer_rsrc_t none; // num_records = 0: every load reads 0 (rows off the frame)
     uint32_t W, H;
     int ylast;                   // last row the unit needs: later prefetches read nothing
     int tail_row;                // EXACT: rows >= tail_row may have windows crossing W * H
@@ -150,8 +151,13 @@ __device__ __forceinline__ typename LaneRow<LC>::type load_row(const RowSource& 
             return r;
         }
     }
-    if constexpr (LC == 16)
-        return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b128(src.rs, o, 0, 0));
+    if constexpr (LC == 16) {
+        // the row offset as the load's scalar offset and the lane's column as its vector
+        // offset (no per-lane add); a row off the frame takes the empty resource instead
+        (void)o;
+        return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b128(
+            in ? src.rs : src.none, xb, in ? y * (int)src.W : 0, 0));
+    }
     else
         return __builtin_bit_cast(RowV, __builtin_amdgcn_raw_buffer_load_b64(src.rs, o, 0, 0));
 }
@@ -1230,6 +1236,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         const_cast<uint8_t*>(img), 0, (int)((W * H + 15) * kPx), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_exact = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(img), 0, (int)(W * H * kPx), 0x00020000);
+    u.src.none = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(img), 0, 0, 0x00020000);
     u.t = P.threshold;
     u.nw = nw;
     u.yb = (int)(y0 - halo);
