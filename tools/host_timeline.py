@@ -40,7 +40,9 @@ def main():
     ev = load(args.dir)
     calls, cur = [], []
     for e in ev:
-        if "HOST_TO_DEVICE" in e[2] and cur:
+        # a call starts at the first host-to-device copy after other work (an overlapped
+        # upload is several copies in a row)
+        if "HOST_TO_DEVICE" in e[2] and cur and "HOST_TO_DEVICE" not in cur[-1][2]:
             calls.append(cur)
             cur = []
         cur.append(e)
