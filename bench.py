@@ -348,10 +348,13 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
     pre-filter), SAD NMS; 128 frames = 1.06 GB, the same bytes per launch as config 4.  Same
     protocol as the headline (timed_steps over `lanes`), plus one lane for the isolated
     kernel."""
+    import torch
+
     W, H = 3840, 2160
     batch = workloads.s1_frames_torch(0, frames, W, H, device=device)
     cfg = Config(8, 12, NonMaximalSuppression.SumAbsolute)
     bufs = LaneBufs(len(lanes), frames * 120_000, frames, device)
+    sum_before = int(batch.sum(dtype=torch.int64))
     t = timed_steps(fast_hip, lanes, bufs, [batch], cfg, steps, warmup, 1, settle=settle)
     lanes1 = fast_hip.Lanes(1, device.index or 0)
     buf1 = LaneBufs.__new__(LaneBufs)
@@ -366,6 +369,7 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
     repeat_ok = all(bool(np.array_equal(bufs.offs[i].cpu().numpy(), o1)) and bool(
         np.array_equal(bufs.out[i][: len(p1)].cpu().numpy(), p1)) for i in range(len(lanes)))
     checked = sorted({0, int(np.argmax(np.diff(o1)))})
+    unchanged = int(batch.sum(dtype=torch.int64)) == sum_before
     exact = all(np.array_equal(p1[o1[f]:o1[f + 1]].astype(np.uint32),
                                oracle_detect(batch[f].cpu().numpy(), 8, 12, 2)) for f in checked)
     res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad",
@@ -381,7 +385,8 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
                            "roofline_frac": round(alg / (float(np.mean(t1.det)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                            if len(t1.det) else None},
            "keypoints_per_step": total,
-           "parity": {"oracle_frames": checked, "bit_exact": exact, "lanes_identical": repeat_ok}}
+           "parity": {"oracle_frames": checked, "bit_exact": exact, "lanes_identical": repeat_ok,
+                      "input_checksum": sum_before, "input_unchanged": unchanged}}
     del batch, bufs
     return res
 
@@ -525,6 +530,9 @@ def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle
     def call(k):
         lanes.detect_device(k, copies[k % len(copies)], cfg, bufs.out[k % n], bufs.offs[k % n],
                             after_current=False)
+
+    # the lanes do not wait on torch's stream: the inputs and buffers it just made must be done
+    torch.cuda.synchronize()
 
     if settle > 0:
         t_end = time.perf_counter() + settle

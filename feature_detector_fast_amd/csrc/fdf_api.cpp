@@ -54,7 +54,8 @@ struct fdf_ctx {
     // chunk's flag (pinned, device-mapped) set to the call's epoch after its copy, while the
     // detector already runs and each band waits for the chunk of its last row
     hipStream_t copy_stream = nullptr;
-    uint32_t* h_flags = nullptr;        uint32_t* hd_flags = nullptr;
+    uint32_t* h_flags = nullptr;        // pinned: the epoch each chunk's flag copy carries
+    uint32_t* d_flags = nullptr;        // device: the chunk flags the bands poll
     uint32_t chunk_epoch = 0;
     uint32_t chunks = 0;                // upload chunks (0: kChunksDefault; 1: no overlap)
     uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
@@ -115,7 +116,10 @@ constexpr size_t kMaxTimedCalls = 4096;
 constexpr uint64_t kDefaultMinTasks = 1024;   // 4 workgroups on each of 256 CUs
 constexpr uint32_t kMaxBandRows = 256;        // fdf_ctx_set_band_rows: the automatic path's range
 constexpr uint32_t kMaxChunks = 16;           // overlapped upload: chunks at most
-constexpr uint32_t kChunksDefault = 4;
+// Default 1 (no overlap): each chunk's ready flag costs a copy on the copy stream, which this
+// runtime runs as a blit kernel (~4 us plus ~9 us of queue gap, profiles/r04/t7_*): 1080p
+// max-t pinned measured p50 0.0787 / 0.0999 / 0.1406 / 0.2196 ms at 1 / 2 / 4 / 8 chunks.
+constexpr uint32_t kChunksDefault = 1;
 constexpr size_t kChunkMinBytes = 1u << 18;   // frames below 256 KB upload in one copy
 
 // process-wide counters: fdf_detect_batch_multi call generations, direct-output launch tags
@@ -317,15 +321,17 @@ int ensure_chunk_flags(fdf_ctx* ctx) {
     if (!ctx->h_flags) {
         void* hp = nullptr;
         void* dp = nullptr;
-        if (hipHostMalloc(&hp, kMaxChunks * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+        if (hipHostMalloc(&hp, kMaxChunks * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
             return FDF_ERR_ALLOC;
-        if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+        if (hipMalloc(&dp, kMaxChunks * sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(dp, 0, kMaxChunks * sizeof(uint32_t)) != hipSuccess) {
             (void)hipHostFree(hp);
+            if (dp) (void)hipFree(dp);
             return FDF_ERR_ALLOC;
         }
         std::memset(hp, 0, kMaxChunks * sizeof(uint32_t));
         ctx->h_flags = static_cast<uint32_t*>(hp);
-        ctx->hd_flags = static_cast<uint32_t*>(dp);
+        ctx->d_flags = static_cast<uint32_t*>(dp);
     }
     return FDF_OK;
 }
@@ -664,7 +670,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                                                     kMaxChunks);
         up.rows = (h + nchunks - 1) / nchunks;
         up.epoch = ++ctx->chunk_epoch == 0 ? ++ctx->chunk_epoch : ctx->chunk_epoch;
-        up.flags = ctx->hd_flags;
+        up.flags = ctx->d_flags;
         for (uint32_t r0 = 0, c = 0; r0 < h; r0 += up.rows, ++c) {
             const uint32_t nr = std::min(up.rows, h - r0);
             const uint8_t* src = data + (size_t)r0 * row_stride;
@@ -674,7 +680,12 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                                                 ctx->copy_stream)
                                : hipMemcpy2DAsync(dst, w, src, row_stride, w, nr,
                                                   hipMemcpyHostToDevice, ctx->copy_stream);
-            if (e == hipSuccess) e = hipStreamWriteValue32(ctx->copy_stream, ctx->hd_flags + c, up.epoch, 0);
+            // the chunk's flag: a 4-byte copy behind it on the same (copy-engine) queue --
+            // hipStreamWriteValue32 is a kernel launch per call on this runtime (~20 us each)
+            ctx->h_flags[c] = up.epoch;
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(ctx->d_flags + c, ctx->h_flags + c, sizeof(uint32_t),
+                                   hipMemcpyHostToDevice, ctx->copy_stream);
             if (e != hipSuccess) {
                 // the runtime cannot do this upload: one copy before the launch, from now on
                 (void)hipStreamSynchronize(ctx->copy_stream);
@@ -943,6 +954,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         if (ctx->h_out) (void)hipHostFree(ctx->h_out);
         if (ctx->h_offs) (void)hipHostFree(ctx->h_offs);
         if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+        (void)hipFree(ctx->d_flags);
         if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
         (void)hipFree(ctx->d_scores);
         (void)hipFree(ctx->d_slots);

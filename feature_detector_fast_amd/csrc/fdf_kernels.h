@@ -208,9 +208,10 @@ struct BandParams {
     uint32_t* lookback_error;
     // Host frames arriving in row chunks while the kernel runs (fdf_detect's overlapped
     // upload; NULL: the frames are in place): chunk c = rows [c * chunk_rows, (c+1) *
-    // chunk_rows) has landed once chunk_flags[c] == chunk_epoch (host-mapped words the copy
-    // stream writes after each chunk's copy, in order).  A band waits for the chunk of the
-    // last row it reads before its first load; a wait that runs out sets lookback_error.
+    // chunk_rows) has landed once chunk_flags[c] == chunk_epoch (device words a 4-byte copy
+    // on the copy stream writes after each chunk's copy, in order).  A band waits for the
+    // chunk of the last row it reads before its first load; a wait that runs out sets
+    // lookback_error.
     const uint32_t* chunk_flags;
     uint32_t chunk_rows;
     uint32_t chunk_epoch;

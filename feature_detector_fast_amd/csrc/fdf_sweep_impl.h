@@ -1199,7 +1199,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         uint32_t* flag = const_cast<uint32_t*>(P.chunk_flags) + last_row / P.chunk_rows;
         for (uint32_t polls = 0;; ++polls) {
             const uint32_t v = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             if (v == P.chunk_epoch) break;
             if (polls > (1u << 20)) {                 // ~30 ms: the copy never landed
                 if (P.lookback_error && lane == 0)

@@ -117,10 +117,11 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
 int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows);
 
 /* Overlapped upload (extension): fdf_detect uploads a frame of >= 256 KB in `chunks` row
- * chunks (default 0 = 4, at most 16) on a copy stream of the context while the detector
- * already runs; each band waits (on the device) for the chunk holding the last row it reads,
- * so the upload overlaps the detection.  chunks = 1: one copy before the launch.  The
- * keypoints are the same either way. */
+ * chunks (at most 16) on a copy stream of the context while the detector already runs; each
+ * band waits (on the device) for the chunk holding the last row it reads.  chunks = 1 (the
+ * default, also 0): one copy before the launch -- on ROCm 7 each chunk's ready flag costs a
+ * small blit launch, so more chunks measured slower.  The keypoints are
+ * the same either way. */
 int fdf_ctx_set_upload_chunks(fdf_ctx* ctx, uint32_t chunks);
 
 /* Device bytes the context's workspace holds now (host-API staging and output, per-band

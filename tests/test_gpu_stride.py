@@ -209,7 +209,7 @@ def test_concurrent_direct_grids_device():
             assert np.array_equal(p0[o0[f]:o0[f + 1]], oracle.detect(hosts[k][f], 16, 9, 1)), (k, f)
 
 
-@pytest.mark.parametrize("chunks", [0, 2, 16, 1])
+@pytest.mark.parametrize("chunks", [4, 2, 16, 1, 0])
 def test_host_overlapped_upload(chunks):
     """fdf_detect's overlapped upload (fdf_ctx_set_upload_chunks): the frame goes up in row
     chunks while the detector runs, each band waiting for the chunk of its last row.  Frames

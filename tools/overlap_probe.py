@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--lanes", default="1,2", help="comma-separated lane counts to time")
     ap.add_argument("--torch-streams", action="store_true", help="also time 2 lanes on torch streams")
     ap.add_argument("--settle", type=float, default=1.0)
+    ap.add_argument("--cap", type=int, default=20_000, help="output points per frame")
     ap.add_argument("--rows", default="0",
                     help="band heights to time (fdf_ctx_set_band_rows on every lane; 0 = automatic)")
     args = ap.parse_args()
@@ -50,7 +51,7 @@ def main():
     L = max(lanes + ([2] if args.torch_streams else []))
     lib = _native.load()
     ctxs = [_native.Context(0) for _ in range(L)]
-    outs = [torch.empty((F * 20_000, 2), dtype=torch.int32, device="cuda") for _ in ctxs]
+    outs = [torch.empty((F * args.cap, 2), dtype=torch.int32, device="cuda") for _ in ctxs]
     offs = [torch.zeros(F + 1, dtype=torch.int64, device="cuda") for _ in ctxs]
     tstreams = [torch.cuda.Stream().cuda_stream for _ in range(2)]
     cfg = _native.FdfConfig(args.threshold, args.count, nms)
@@ -94,10 +95,12 @@ def main():
             torch.cuda.synchronize()
             res[name].append((time.perf_counter() - t0) * 1e3 / args.steps)
     same = all(bool(torch.equal(offs[0], o)) for o in offs[1:])
+    total = int(offs[0][-1])
     print(json.dumps({"frames": F, "shape": f"{W}x{H}", "nms": args.nms, "steps": args.steps,
                       "ms_per_call": {k: round(sorted(v)[len(v) // 2], 4) for k, v in res.items()},
                       "ms_per_call_all": {k: [round(x, 4) for x in sorted(v)] for k, v in res.items()},
-                      "outputs_equal": same}))
+                      "outputs_equal": same, "points": total,
+                      "points_fit": total <= outs[0].shape[0]}))
     for c in ctxs:
         c.close()
 
