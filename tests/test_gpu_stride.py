@@ -234,3 +234,32 @@ def test_host_overlapped_upload(chunks):
                 assert np.array_equal(got, want[(i, nms)]), (rep, i, nms)
     finally:
         ctx.set_upload_chunks(0)
+
+
+def test_context_setter_bounds():
+    """fdf_ctx_set_band_rows rejects heights past the automatic range (256; the
+    LDS layout arithmetic would overflow far beyond it) and fdf_ctx_set_upload_chunks more
+    than 16 chunks, with FDF_ERR_ARG and the context unchanged."""
+    ctx = _native.Context(0)
+    try:
+        for bad in (257, 1 << 30, 0xFFFFFFFF):
+            with pytest.raises(_native.FdfError) as e:
+                ctx.set_band_rows(bad)
+            assert e.value.status == _native.FDF_ERR_ARG
+        with pytest.raises(_native.FdfError) as e:
+            ctx.set_upload_chunks(17)
+        assert e.value.status == _native.FDF_ERR_ARG
+        ctx.set_band_rows(256)
+        import torch
+
+        img = workloads.s1_frame(3)
+        frames = torch.from_numpy(img[None].copy()).cuda()
+        out = torch.empty((200_000, 2), dtype=torch.int32, device="cuda")
+        offs = torch.zeros(2, dtype=torch.int64, device="cuda")
+        fast_hip.detect_device(frames, Config(16, 9, NonMaximalSuppression.MaxThreshold), out,
+                               offs, ctx=ctx)
+        torch.cuda.synchronize()
+        got = out[: int(offs[1])].cpu().numpy().astype(np.uint32)
+        assert np.array_equal(got, oracle.detect(img, 16, 9, 1))
+    finally:
+        ctx.close()

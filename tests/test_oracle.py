@@ -456,3 +456,18 @@ def test_input_image_is_compare_rs_luma(tmp_path):
     Image.fromarray(col).save(p2)
     grey2, _ = workloads.input_image(str(p2))
     assert np.array_equal(grey2, oracle.rgb_to_luma(col))
+
+
+def test_load_rgb_rejects_wide_modes(tmp_path):
+    """a 16-bit PNG is not silently clipped to 8 bits (image 0.24's to_rgb8
+    scales it); load_rgb refuses modes other than 8-bit channels."""
+    from PIL import Image
+
+    p = tmp_path / "wide.png"
+    Image.fromarray(np.arange(64 * 48, dtype=np.uint16).reshape(48, 64) * 20, mode="I;16").save(p)
+    with pytest.raises(ValueError, match="8-bit"):
+        workloads.load_rgb(str(p))
+    q = tmp_path / "grey.png"
+    Image.fromarray(np.arange(64 * 48, dtype=np.uint8).reshape(48, 64)).save(q)
+    rgb = workloads.load_rgb(str(q))
+    assert rgb.shape == (48, 64, 3) and np.array_equal(rgb[..., 0], rgb[..., 2])
