@@ -30,6 +30,8 @@ struct LastResult {
     uint32_t n_frames = 0, width = 0, height = 0;
     fdf_config cfg{};
     bool rgb = false;              // frames in d_rgb (RGB8); scores need their luma in d_in
+    bool in_place = false;         // the frame was read in place from pinned host memory: not
+                                   // in d_in, so the result has no scores (fdf_fetch_last)
     // fdf_detect_batch_multi: the call's generation (0: not a multi-context result) and this
     // context's shard of it, checked by fdf_fetch_last_multi
     uint64_t multi_gen = 0;
@@ -665,7 +667,27 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
 #endif
     const bool chunked = host_out && !rgb && n_frames == 1 && frame_bytes >= kChunkMinBytes &&
                          ctx->chunks != 1 && ctx->h_stats && ensure_chunk_flags(ctx) == FDF_OK;
-    if (chunked) {
+    // one packed grey frame in pinned (page-locked, non-coherent) host memory, unscored: the
+    // detector reads it in place over PCIe, with no copy before the launch -- its row stream
+    // is the upload (1080p max-t 72-75 vs 82-83 us end to end).  Host writes
+    // to the buffer before the call are visible to the launch (the dispatch's system-scope
+    // acquire; a wave-level acquire fence cost ~20 us and changed no result:
+    // tests/test_gpu_host_inplace.py reuses one buffer for different frames).  The frame is
+    // then not in d_in: a result that does not fit the caller's buffer copies it there for
+    // fdf_fetch_last (detect_host).
+    const uint8_t* in_place = nullptr;
+    if (ctx->chunks == 0 && host_out && !rgb && n_frames == 1 && row_stride == w) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, data) == hipSuccess) {
+            if (a.type == hipMemoryTypeHost && a.devicePointer &&
+                !(a.allocationFlags & hipHostMallocCoherent))
+                in_place = static_cast<const uint8_t*>(a.devicePointer);
+        } else {
+            (void)hipGetLastError();   // pageable memory: not an error here
+        }
+    }
+    if (in_place) {
+    } else if (chunked) {
         const uint32_t nchunks = std::min<uint32_t>(ctx->chunks ? ctx->chunks : kChunksDefault,
                                                     kMaxChunks);
         up.rows = (h + nchunks - 1) / nchunks;
@@ -713,8 +735,8 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
-    rc = enqueue(ctx, ctx->d_in, n_frames, w, h, frame_bytes, cfg, out_dev, *out_cap, offs_dev,
-                 ctx->stream, false, up);
+    rc = enqueue(ctx, in_place ? in_place : ctx->d_in, n_frames, w, h, frame_bytes, cfg,
+                 out_dev, *out_cap, offs_dev, ctx->stream, false, up);
     if (chunked) {
         // the copies end before the detector does (it waits for the last one), but a failed
         // launch or a timed-out wait would leave them running: drain them before any return
@@ -784,6 +806,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     ctx->last.height = h;
     ctx->last.cfg = *cfg;
     ctx->last.rgb = false;          // the luma frames are in d_in
+    ctx->last.in_place = in_place != nullptr;   // ... or were read in place (not in d_in)
     return FDF_OK;
 }
 
@@ -792,6 +815,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
 int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
     if (!n) return FDF_OK;
     const LastResult& L = ctx->last;
+    if (out_scores && L.in_place) return FDF_ERR_ARG;
     hipError_t e = hipSuccess;
     if (out_scores) {
         int rc = ensure(ctx, &ctx->d_scores, &ctx->scores_n, n, ctx->stream);
@@ -858,6 +882,14 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
     rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored);
     if (rc) return rc;
     const uint64_t total = offs[n_frames];
+    if (total > cap && ctx->last.in_place) {
+        // the two-call pattern follows: keep the frame for fdf_fetch_last's scores
+        if (hipMemcpyAsync(ctx->d_in, data, (size_t)w * h, hipMemcpyHostToDevice, ctx->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return FDF_ERR_DEVICE;
+        ctx->last.in_place = false;
+    }
     rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
     if (rc) return rc;
     *n_out = (size_t)total;

@@ -116,12 +116,14 @@ int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks);
  * the automatic choice's range): FDF_ERR_ARG. */
 int fdf_ctx_set_band_rows(fdf_ctx* ctx, uint32_t rows);
 
-/* Overlapped upload (extension): fdf_detect uploads a frame of >= 256 KB in `chunks` row
- * chunks (at most 16) on a copy stream of the context while the detector already runs; each
- * band waits (on the device) for the chunk holding the last row it reads.  chunks = 1 (the
- * default, also 0): one copy before the launch -- on ROCm 7 each chunk's ready flag costs a
- * small blit launch, so more chunks measured slower.  The keypoints are
- * the same either way. */
+/* How fdf_detect gets a host frame to the device (extension).  chunks = 0 (default): a
+ * packed frame (stride = width) in pinned, non-coherent host memory (hipHostMalloc /
+ * hipHostRegister without the coherent flag) is read in place by the detector over PCIe, no
+ * copy first; any other frame is copied before the launch.  chunks = 1: always one copy.
+ * chunks = k in 2..16: a frame of >= 256 KB goes up in k row chunks on a copy stream while
+ * the detector already runs, each band waiting (on the device) for the chunk holding the last
+ * row it reads -- on ROCm 7 each chunk's ready flag costs a small blit launch, so this
+ * measured slower.  The keypoints are the same either way. */
 int fdf_ctx_set_upload_chunks(fdf_ctx* ctx, uint32_t chunks);
 
 /* Device bytes the context's workspace holds now (host-API staging and output, per-band
@@ -147,7 +149,9 @@ int fdf_detect(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t heigh
  * and the scored variants), and their scores when `out_scores` is not NULL (the score kind
  * of that call's config, as fdf_detect_scored).  Only copies: no detection runs.
  * FDF_ERR_CAPACITY again if `cap` < *n_out; FDF_ERR_ARG if the context holds no result
- * (no host detection yet, or fdf_score_points ran since).
+ * (no host detection yet, or fdf_score_points ran since), or if scores are asked of an
+ * unscored fdf_detect that fit its `cap` and read its pinned frame in place (the frame is not
+ * kept; fdf_ctx_set_upload_chunks) -- a call that returned FDF_ERR_CAPACITY keeps it.
  */
 int fdf_fetch_last(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t cap,
                    size_t* n_out);

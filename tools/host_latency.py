@@ -23,7 +23,9 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--chunks", default="0,1",
-                    help="fdf_ctx_set_upload_chunks values to time (0 = default overlap, 1 = none)")
+                    help="fdf_ctx_set_upload_chunks values to time (0 = default, 1 = one copy)")
+    ap.add_argument("--rows", default="0",
+                    help="fdf_ctx_set_band_rows values to time (0 = automatic)")
     args = ap.parse_args()
     import torch
 
@@ -39,11 +41,13 @@ def main():
     pin_out = torch.empty((cap, 2), dtype=torch.int32).pin_memory()
     np_out = np.empty((cap, 2), dtype=np.uint32)
     res = {}
-    for name, mem, ch in [(n, m, c) for n in args.modes.split(",") for m in args.mem.split(",")
-                          for c in args.chunks.split(",")]:
+    for name, mem, ch, rows in [(n, m, c, r) for n in args.modes.split(",")
+                                for m in args.mem.split(",") for c in args.chunks.split(",")
+                                for r in args.rows.split(",")]:
         mode = {"off": 0, "maxt": 1, "sad": 2}[name]
         c = _native.FdfConfig(16, 9, mode)
         ctx.set_upload_chunks(int(ch))
+        ctx.set_band_rows(int(rows))
         src, dst = ((pin_in.data_ptr(), pin_out.data_ptr()) if mem == "pinned"
                     else (frame.ctypes.data, np_out.ctypes.data))
         n = ctypes.c_size_t(0)
@@ -58,8 +62,11 @@ def main():
                 ts.append((t1 - t0) * 1e3)
         ts = np.sort(ts)
         q = lambda p: round(float(ts[int(p * (len(ts) - 1))]), 4)
-        key = f"{name}_{mem}" + ("" if ch == "0" else f"_chunks{ch}")
+        key = (f"{name}_{mem}" + ("" if ch == "0" else f"_chunks{ch}") +
+               ("" if rows == "0" else f"_rows{rows}"))
         res[key] = {"p5": q(0.05), "p50": q(0.5), "p95": q(0.95), "keypoints": n.value}
+    ctx.set_band_rows(0)
+    ctx.set_upload_chunks(0)
     print(json.dumps(res))
 
 
