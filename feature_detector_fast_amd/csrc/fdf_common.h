@@ -40,6 +40,14 @@ __device__ __forceinline__ uint32_t lanes_below_plus(uint64_t mask, uint32_t bas
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, base));
 }
+// The v_bitop3 truth table of f(a, b, c): bit (a << 2 | b << 1 | c) = f(a, b, c).
+template <typename F>
+__host__ __device__ constexpr uint32_t lut3(F f) {
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i)
+        if (f((i >> 2) & 1, (i >> 1) & 1, i & 1)) r |= 1u << i;
+    return r;
+}
 // sel ? a : b, bit by bit, in one v_bitop3 (LUT 0xCA: src0 selects src1 over src2)
 __device__ __forceinline__ uint32_t bitop3_sel(uint32_t sel, uint32_t a, uint32_t b) {
     return __builtin_amdgcn_bitop3_b32(sel, a, b, 0xCA);
@@ -105,12 +113,39 @@ __device__ __forceinline__ bool run_of(uint32_t m) {
     return (m & 0xffffu) != 0;
 }
 
-// Bit 7 of byte j of f[m] is the flag of circle pixel 4j + m -> the doubled circle mask.
-__device__ __forceinline__ uint32_t gather_flags(const uint32_t (&f)[4]) {
-    uint32_t x = ((f[0] >> 7) & 0x01010101u) | ((f[1] >> 6) & 0x02020202u) |
-                 ((f[2] >> 5) & 0x04040404u) | ((f[3] >> 4) & 0x08080808u);  // pixel 4j+m: bit 8j+m
-    x |= x >> 4;                                         // pixels 0..7 in byte 0, 8..15 in byte 2
-    return __builtin_amdgcn_perm(x, x, 0x02000200u);     // bytes [b0, b2, b0, b2]
+// Bit 7 of byte j of f[m] is the flag of circle pixel 4j + m -> pixels 0..7 in byte 1 and
+// 8..15 in byte 3 (pixel i at bit 8 + i, resp. 24 + i - 8), of the flags or (INV) of their
+// inverses: the flags go to bits 7..4 of each byte by masked selects (zero below), then
+// each byte's nibble joins the next byte's: 8 VALU, the inversion in the select tables.
+template <bool INV>
+__device__ __forceinline__ uint32_t gather_ring(const uint32_t (&f)[4]) {
+    constexpr uint32_t kSel = lut3([](int s, int a, int b) { return s ? (INV ? !a : a) : b; });
+    constexpr uint32_t kTop = lut3([](int s, int a, int) { return s && (INV ? !a : a); });
+    uint32_t t = __builtin_amdgcn_bitop3_b32(0x80808080u, f[3], 0u, kTop);
+    t = __builtin_amdgcn_bitop3_b32(0x40404040u, f[2] >> 1, t, kSel);
+    t = __builtin_amdgcn_bitop3_b32(0x20202020u, f[1] >> 2, t, kSel);
+    t = __builtin_amdgcn_bitop3_b32(0x10101010u, f[0] >> 3, t, kSel);
+    return t | (t << 4);
+}
+
+// Runs of >= N in two 16-bit cyclic rings at once (bright in bits 0-15, dark in 16-31):
+// bit i of a half ANDed with the half rotated right by 1, 2, 4 and N - 8 (packed 16-bit
+// shifts), so bit i ends as "flags i .. i + N - 1 of that ring all set".
+template <int N>
+__device__ __forceinline__ uint32_t runs16x2(uint32_t m) {
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t kAndOr = lut3([](int a, int b, int c) { return a && (b || c); });
+    auto step = [&](uint32_t x, uint16_t s) {
+        const u16x2 v = __builtin_bit_cast(u16x2, x);
+        const u16x2 hi = v >> (u16x2)(s), lo = v << (u16x2)((uint16_t)(16 - s));
+        return __builtin_amdgcn_bitop3_b32(x, __builtin_bit_cast(uint32_t, hi),
+                                           __builtin_bit_cast(uint32_t, lo), kAndOr);
+    };
+    m = step(m, 1);
+    m = step(m, 2);
+    m = step(m, 4);
+    if constexpr (N > 8) m = step(m, N - 8);
+    return m;
 }
 
 // Bright / dark runs of >= N (src/fast_simd.rs:115-297) on the ring packed 4 bytes per word
@@ -126,8 +161,12 @@ __device__ __forceinline__ void lane_segment_test_packed(uint32_t c, const uint3
         fb[m] = lerp_u8(lerp_u8(w[m], nc, k.rb), k.kb, 0);   // p - c > t
         fn[m] = lerp_u8(lerp_u8(w[m], nc, k.rd), k.kd, 0);   // NOT(p - c < -t)
     }
-    bright = run_of<N>(gather_flags(fb));
-    dark = run_of<N>(~gather_flags(fn));
+    // bright ring in bits 0-15, dark (inverted fn) in bits 16-31: bytes 1 and 3 of each
+    const uint32_t rings = __builtin_amdgcn_perm(gather_ring<true>(fn), gather_ring<false>(fb),
+                                                 0x07050301u);
+    const uint32_t m = runs16x2<N>(rings);
+    bright = (m & 0xffffu) != 0;
+    dark = m > 0xffffu;
 }
 
 // The same on 16 separate ring bytes.

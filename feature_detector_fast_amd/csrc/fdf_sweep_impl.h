@@ -659,8 +659,24 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                     br = (bn | bs) & (be | bw);                                              \
                     nd = (dn & ds) | (de & dw);                                              \
                 } else {                                                                     \
-                    br = (bn & bs & (be | bw)) | (be & bw & (bn | bs));                      \
-                    nd = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw));                    \
+                    /* >= 3 of 4 bright = and3(n,s,e) | (maj3(n,s,e) & w); NOT dark = >= 2 */  \
+                    /* of 4 not-dark = maj3(n,s,e) | (or3(n,s,e) & w): six v_bitop3 on the */  \
+                    /* raw flag words (inversions in the tables) where the compiler made 10 */ \
+                    constexpr uint32_t kMaj = lut3([](int a, int b, int c) {                \
+                        return (!a + b + c) >= 2; });                                        \
+                    constexpr uint32_t kAnd = lut3([](int a, int b, int c) {                \
+                        return !a && b && c; });                                             \
+                    constexpr uint32_t kOr = lut3([](int a, int b, int c) {                 \
+                        return !a || b || c; });                                             \
+                    constexpr uint32_t kJoin = lut3([](int a, int b, int c) {               \
+                        return a || (b && !c); });                                           \
+                    const uint32_t m1 = __builtin_amdgcn_bitop3_b32(vn.nd[m], bs, be, kMaj); \
+                    const uint32_t t1 = __builtin_amdgcn_bitop3_b32(vn.nd[m], bs, be, kAnd); \
+                    br = __builtin_amdgcn_bitop3_b32(t1, m1, hndw, kJoin);                   \
+                    const uint32_t m2 = __builtin_amdgcn_bitop3_b32(vn.b[m], ds, de, kMaj);  \
+                    const uint32_t o2 = __builtin_amdgcn_bitop3_b32(vn.b[m], ds, de, kOr);   \
+                    nd = __builtin_amdgcn_bitop3_b32(m2, o2, hbw, kJoin);                    \
+                    (void)bn; (void)bw; (void)dn; (void)dw;                                  \
                 }                                                                            \
                 cand[m] = br | ~nd;                                                          \
             }                                                                                \
