@@ -213,41 +213,52 @@ def test_s2_1080p_counts():
     assert len(oracle.detect(img, 16, 12, 0)) == 0
 
 
-def _lane_segment_test(c, ring, t, n):
-    """numpy restatement of fdf_common.h lane_segment_test: bytes packed 4 per word (byte j
-    of word m = pixel 4j + m), lerp SWAR compares, flags gathered into the doubled circle
-    mask with the kernel's shift / fold / byte-permute, then the doubling-AND run test."""
+def _lane_segment_test(c, ring, t, n, rng=None):
+    """numpy restatement of fdf_common.h lane_segment_test_packed: bytes packed 4 per word
+    (byte j of word m = pixel 4j + m), lerp SWAR compares (only bit 7 of each byte is a flag;
+    the other bits are filled with noise here, as the lerps leave them), each polarity's flags
+    gathered by masked bitop3 selects (gather_ring; the dark side inverted in the tables), the
+    two rings joined into one word by v_perm (bright bits 0-15, dark 16-31), then the run test
+    of both rings at once with packed 16-bit rotations (runs16x2)."""
     ob, od = t & 1, (t + 1) & 1
     kb = 128 - ((t + ob) >> 1)
     kd = 255 - ((254 - t + od) >> 1)
     ring = np.asarray(ring)
+    M = 0xffffffff
 
     def word_flags(r, k):
         fl = [0, 0, 0, 0]
         for m in range(4):
             for j in range(4):
                 v = _lerp(_lerp(np.array(ring[4 * j + m]), np.array(255 - c), r), np.array(k), 0)
-                fl[m] |= (int(v) & 0x80) << (8 * j)
+                noise = int(rng.integers(0, 128)) if rng is not None else 0
+                fl[m] |= ((int(v) & 0x80) | noise) << (8 * j)
         return fl
 
-    def gather(f):
-        x = (((f[0] >> 7) & 0x01010101) | ((f[1] >> 6) & 0x02020202) |
-             ((f[2] >> 5) & 0x04040404) | ((f[3] >> 4) & 0x08080808))
-        x |= x >> 4
-        b0, b2 = x & 0xff, (x >> 16) & 0xff
-        return b0 | (b2 << 8) | (b0 << 16) | (b2 << 24)
+    def sel(s, a, b):
+        return ((s & a) | (~s & b)) & M
 
-    def run(m):
-        m &= m >> 1
-        m &= m >> 2
-        m &= m >> 4
-        if n > 8:
-            m &= m >> (n - 8)
-        return (m & 0xffff) != 0
+    def gather_ring(f, inv):
+        g = (lambda x: ~x & M) if inv else (lambda x: x)
+        tt = g(f[3]) & 0x80808080
+        tt = sel(0x40404040, g(f[2] >> 1), tt)
+        tt = sel(0x20202020, g(f[1] >> 2), tt)
+        tt = sel(0x10101010, g(f[0] >> 3), tt)
+        return (tt | (tt << 4)) & M
 
-    bright = run(gather(word_flags(ob, kb)))
-    dark = run(~gather(word_flags(od, kd)) & 0xffffffff)
-    return bright, dark
+    def rot16x2(m, sh):
+        r = lambda v: ((v >> sh) | (v << (16 - sh))) & 0xffff
+        return r(m & 0xffff) | (r(m >> 16) << 16)
+
+    def runs16x2(m):
+        for sh in [1, 2, 4] + ([n - 8] if n > 8 else []):
+            m = m & (rot16x2(m, sh))
+        return m
+
+    rings = _perm(gather_ring(word_flags(od, kd), True), gather_ring(word_flags(ob, kb), False),
+                  0x07050301)
+    m = runs16x2(rings)
+    return (m & 0xffff) != 0, m > 0xffff
 
 
 def test_lane_segment_test_matches_oracle():
@@ -265,7 +276,7 @@ def test_lane_segment_test_matches_oracle():
                 ring[(s0 + q) % 16] = hi[q]
         else:
             ring = rng.integers(0, 256, 16)
-        b, d = _lane_segment_test(c, ring.tolist(), t, n)
+        b, d = _lane_segment_test(c, ring.tolist(), t, n, rng)
         bright = [p > c + t for p in ring]
         dark = [p < c - t for p in ring]
         assert b == _consecutive(bright, n) and d == _consecutive(dark, n), (c, t, n, ring)
@@ -471,3 +482,39 @@ def test_load_rgb_rejects_wide_modes(tmp_path):
     Image.fromarray(np.arange(64 * 48, dtype=np.uint8).reshape(48, 64)).save(q)
     rgb = workloads.load_rgb(str(q))
     assert rgb.shape == (48, 64, 3) and np.array_equal(rgb[..., 0], rgb[..., 2])
+
+
+def test_three_of_four_prefilter_tables():
+    """fdf_sweep_impl.h, n >= 12: the 3-of-4 cardinal pre-filter as six v_bitop3 on the raw
+    flag words (and3 | maj3 & w for bright; maj3 | or3 & w for not-dark, inversions in the
+    tables) equals the reference's formula (src/fast_simd.rs:441-509) bit for bit."""
+    M = 0xffffffff
+
+    def lut3(f):
+        return sum(1 << i for i in range(8) if f((i >> 2) & 1, (i >> 1) & 1, i & 1))
+
+    def bitop3(a, b, c, lut):
+        out = 0
+        for bit in range(32):
+            i = (((a >> bit) & 1) << 2) | (((b >> bit) & 1) << 1) | ((c >> bit) & 1)
+            out |= ((lut >> i) & 1) << bit
+        return out
+
+    k_maj = lut3(lambda a, b, c: (1 - a + b + c) >= 2)
+    k_and = lut3(lambda a, b, c: (not a) and b and c)
+    k_or = lut3(lambda a, b, c: (not a) or b or c)
+    k_join = lut3(lambda a, b, c: a or (b and not c))
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        vn_nd, vs_b, h_b, hndw, vn_b, vs_nd, h_nd, hbw = (int(v) for v in rng.integers(0, 1 << 32, 8))
+        bn, bs, be, bw = ~vn_nd & M, vs_b, h_b, ~hndw & M
+        dn, ds, de, dw = ~vn_b & M, vs_nd, h_nd, ~hbw & M
+        br_ref = (bn & bs & (be | bw)) | (be & bw & (bn | bs))
+        nd_ref = (dn & ds) | (de & dw) | ((dn | ds) & (de | dw))
+        m1 = bitop3(vn_nd, vs_b, h_b, k_maj)
+        t1 = bitop3(vn_nd, vs_b, h_b, k_and)
+        br = bitop3(t1, m1, hndw, k_join)
+        m2 = bitop3(vn_b, vs_nd, h_nd, k_maj)
+        o2 = bitop3(vn_b, vs_nd, h_nd, k_or)
+        nd = bitop3(m2, o2, hbw, k_join)
+        assert br == br_ref and nd == nd_ref
