@@ -112,3 +112,55 @@ def test_in_place_two_call_pattern_keeps_scores():
         assert np.array_equal(out, want)
     finally:
         ctx.close()
+
+
+def _hip():
+    """The HIP runtime already in the process (the one libfdf.so and torch use), never a
+    second copy."""
+    import os
+
+    _native.load()
+    hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_NOW)
+    for fn in ("hipHostMalloc", "hipHostRegister", "hipHostFree", "hipHostUnregister"):
+        getattr(hip, fn).restype = ctypes.c_int
+    return hip
+
+
+@pytest.mark.parametrize("kind", ["coherent", "registered"])
+def test_in_place_other_pinned_kinds(kind):
+    """Fine-grained (coherent) pinned memory is copied, not read in place; memory registered
+    with hipHostRegister is read in place.  Either way the lists equal the oracle, across
+    frames written into the same buffer."""
+    W, H = 1280, 720
+    frames = [workloads.s1_frame(3, W, H), workloads.s3_frame(7)[:H, :W].copy(),
+              workloads.s1_frame(40, W, H)]
+    hip = _hip()
+    ptr = ctypes.c_void_p()
+    keep = None
+    if kind == "coherent":
+        assert hip.hipHostMalloc(ctypes.byref(ptr), ctypes.c_size_t(W * H),
+                                 ctypes.c_uint(0x40000000)) == 0
+        view = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
+    else:
+        keep = np.zeros(W * H + 4096, dtype=np.uint8)
+        base = keep.ctypes.data + (-keep.ctypes.data) % 4096   # page-aligned start
+        view = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
+        assert hip.hipHostRegister(ctypes.c_void_p(base), ctypes.c_size_t(W * H),
+                                   ctypes.c_uint(0)) == 0
+        ptr = ctypes.c_void_p(base)
+    lib = _native.load()
+    ctx = _native.Context(0)
+    try:
+        for rep in range(2):
+            for i, f in enumerate(frames):
+                nms = (i + rep) % 3
+                view[:] = f.reshape(-1)
+                rc, got, _ = _detect(lib, ctx, ptr.value, W, H, 16, 9, nms)
+                _native.check(rc, "fdf_detect")
+                assert np.array_equal(got, oracle.detect(f, 16, 9, nms)), (kind, rep, i, nms)
+    finally:
+        ctx.close()
+        if kind == "coherent":
+            assert hip.hipHostFree(ptr) == 0
+        else:
+            assert hip.hipHostUnregister(ptr) == 0
