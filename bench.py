@@ -14,8 +14,10 @@ one-stream protocol of rounds 1-3).
 
 Besides the headline value the line carries: the roofline of the detector (HIP events on the
 lane streams; algorithmic bytes = W*H + 8*K + 4 per frame), single-frame
-latencies, a parity check of sampled frames against the CPU oracle, and the CPU baseline
-(the AVX2 port of the reference path, oracle/fast_avx2.cpp, rank 0, N=1).
+latencies, whole-batch parity (every frame of every input copy against the CPU checker, on
+every rank, all-reduced), and the CPU baseline (the AVX2 port of the reference path,
+oracle/fast_avx2.cpp, rank 0, N=1).  Each lane reads its own copy of the batch (different
+rolls of the S1 frames), so no two launches in flight share input bytes.
 """
 import argparse
 import json
@@ -57,7 +59,9 @@ def parse_args(argv=None):
     p.add_argument("--nms", choices=sorted(NMS_NAMES), default="maxt")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="budget for the single-thread CPU baseline sample (0 = skip)")
-    p.add_argument("--no-extras", action="store_true", help="skip latency/parity extras")
+    p.add_argument("--no-extras", action="store_true", help="skip the latency/leg extras")
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip the whole-batch parity check of the headline (experiments only)")
     p.add_argument("--lanes", type=int, default=3,
                    help="launch lanes: step k runs on lane k %% L, each lane a context with its "
                         "own HIP stream and no dependency between lanes (fast_hip.Lanes)")
@@ -342,7 +346,7 @@ def host_latency(fast_hip, _native, frame, cfgs, samples=50):
     return res
 
 
-def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device, oracle_detect,
+def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device,
                frames=128, steps=10, warmup=3, settle=0.0):
     """BASELINE.json config 5 on this GPU: 3840x2160 S1 frames, t=8 n=12 (3-of-4 cardinal
     pre-filter), SAD NMS; 128 frames = 1.06 GB, the same bytes per launch as config 4.  Same
@@ -350,44 +354,47 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
     kernel."""
     import torch
 
+    from oracle import oracle
+
     W, H = 3840, 2160
-    batch = workloads.s1_frames_torch(0, frames, W, H, device=device)
+    copies = make_batch(workloads, 0, frames, W, H, device, lanes=len(lanes))
     cfg = Config(8, 12, NonMaximalSuppression.SumAbsolute)
     bufs = LaneBufs(len(lanes), frames * 120_000, frames, device)
-    sum_before = int(batch.sum(dtype=torch.int64))
-    t = timed_steps(fast_hip, lanes, bufs, [batch], cfg, steps, warmup, 1, settle=settle)
+    sums_before = [int(c.sum(dtype=torch.int64)) for c in copies]
+    t = timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, 1, settle=settle)
+    # parity outside the timed region: every frame of every copy against the CPU checker
+    parity, kp_step = batch_parity(oracle, copies, bufs, t, 8, 12, 2, W)
     lanes1 = fast_hip.Lanes(1, device.index or 0)
     buf1 = LaneBufs.__new__(LaneBufs)
     buf1.out, buf1.offs = bufs.out[:1], bufs.offs[:1]
-    t1 = timed_steps(fast_hip, lanes1, buf1, [batch], cfg, steps, warmup, 1)
-    alg = frames * W * H
-    # parity outside the timed regions: every lane's last result equals the one-lane run's,
-    # and frame 0 and the densest frame equal the CPU oracle
-    o1 = bufs.offs[0].cpu().numpy().copy()
-    total = int(o1[-1])
-    p1 = bufs.out[0][: min(total, bufs.out[0].shape[0])].cpu().numpy().copy()
-    repeat_ok = all(bool(np.array_equal(bufs.offs[i].cpu().numpy(), o1)) and bool(
-        np.array_equal(bufs.out[i][: len(p1)].cpu().numpy(), p1)) for i in range(len(lanes)))
-    checked = sorted({0, int(np.argmax(np.diff(o1)))})
-    unchanged = int(batch.sum(dtype=torch.int64)) == sum_before
-    exact = all(np.array_equal(p1[o1[f]:o1[f + 1]].astype(np.uint32),
-                               oracle_detect(batch[f].cpu().numpy(), 8, 12, 2)) for f in checked)
-    res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad",
-           "Mpix_s": round(alg * steps / t.elapsed / 1e6, 1),
+    t1 = timed_steps(fast_hip, lanes1, buf1, copies, cfg, steps, warmup, 1)
+    parity["input_checksums"] = sums_before
+    parity["inputs_unchanged"] = [int(c.sum(dtype=torch.int64)) for c in copies] == sums_before
+    in_bytes = frames * W * H
+    # algorithmic bytes as the headline's (SURVEY.md §8d): W*H + 8K + 4 per frame
+    alg = in_bytes + 8 * kp_step + 4 * frames
+    per_launch = t.span_ms / steps
+    det1 = float(np.mean(t1.det)) if len(t1.det) else None
+    res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad, "
+                       f"{len(copies)} distinct copies (one per lane)",
+           "Mpix_s": round(in_bytes * steps / t.elapsed / 1e6, 1),
            "ms_per_step": round(t.elapsed * 1e3 / steps, 4),
-           "lanes": t.lanes,
-           "kernel_ms_avg": round(t.span_ms / steps, 4),
+           "lanes": t.lanes, "hbm_copies": len(copies),
+           "kernel_ms_avg": round(per_launch, 4),
            "launch_ms_avg": round(float(np.mean(t.det)), 4) if len(t.det) else None,
-           "roofline_frac": round(alg / (t.span_ms / steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "launch_ms": percentiles(t.det) if len(t.det) >= MIN_TIMED else None,
+           "alg_bytes_per_launch": int(round(alg)),
+           "roofline_frac": round(alg / (per_launch * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "roofline_frac_input_bytes_only": round(in_bytes / (per_launch * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "single_lane": {"ms_per_step": round(t1.elapsed * 1e3 / steps, 4),
-                           "kernel_ms_avg": round(float(np.mean(t1.det)), 4) if len(t1.det) else None,
+                           "kernel_ms_avg": round(det1, 4) if det1 else None,
+                           "kernel_ms": percentiles(t1.det) if len(t1.det) >= MIN_TIMED else None,
                            "compaction_kernel_ms_avg": round(float(np.mean(t1.com)), 4) if len(t1.com) else None,
-                           "roofline_frac": round(alg / (float(np.mean(t1.det)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                           if len(t1.det) else None},
-           "keypoints_per_step": total,
-           "parity": {"oracle_frames": checked, "bit_exact": exact, "lanes_identical": repeat_ok,
-                      "input_checksum": sum_before, "input_unchanged": unchanged}}
-    del batch, bufs
+                           "roofline_frac": round(alg / (det1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                           if det1 else None},
+           "keypoints_per_step": int(round(kp_step)),
+           "parity": parity}
+    del copies, bufs
     return res
 
 
@@ -482,15 +489,26 @@ def input_file_checks(fast_hip, Config, NonMaximalSuppression, workloads, oracle
     return res
 
 
-def make_batch(workloads, first, count, W, H, device, min_bytes=0):
-    """`count` S1 frames from global index `first`, plus identical copies until the copies
-    together hold >= min_bytes: a step reads copy k % len(copies), so a shard smaller than
-    the 256 MiB Infinity Cache is still read from HBM on every step."""
-    batch = workloads.s1_frames_torch(first, count, W, H, device=device)
-    copies = [batch]
-    while min_bytes and len(copies) * batch.numel() < min_bytes:
-        copies.append(batch.clone())
-    return copies
+COPY_ROLL = 211   # copy c's frame k is S1 frame first + k + 211 c (a different roll)
+
+
+def n_copies(batch_bytes, lanes, min_bytes):
+    """Distinct input copies of a shard: at least one per lane, so no two launches in flight
+    read the same bytes, enough to hold >= min_bytes together (a shard
+    smaller than the 256 MiB Infinity Cache is still read from HBM on every step), and a
+    multiple of the lane count, so lane i always reads copies i, i + L, ..."""
+    need = max(1, -(-min_bytes // max(1, batch_bytes))) if min_bytes else 1
+    need = max(need, lanes)
+    return -(-need // lanes) * lanes
+
+
+def make_batch(workloads, first, count, W, H, device, min_bytes=0, lanes=1):
+    """`count` S1 frames from global index `first` in n_copies(...) distinct copies: copy c
+    holds frames first + 211 c ... (each frame rolled differently from the same position in
+    every other copy).  Step k reads copy k % len(copies) on lane k % lanes."""
+    nc = n_copies(count * W * H, lanes, min_bytes)
+    return [workloads.s1_frames_torch(first + COPY_ROLL * c, count, W, H, device=device)
+            for c in range(nc)]
 
 
 class LaneBufs:
@@ -510,9 +528,14 @@ class Timed:
     the per-launch detector / compaction durations the library's dispatches timestamped, and
     the lane that ran the last step (its buffers hold the last result)."""
 
-    def __init__(self, elapsed, span_ms, det, com, last, steps, lanes):
+    def __init__(self, elapsed, span_ms, det, com, last, steps, lanes, lane_copy=None,
+                 copy_steps=None):
         self.elapsed, self.span_ms, self.det, self.com = elapsed, span_ms, det, com
         self.last, self.steps, self.lanes = last, steps, lanes
+        # lane -> the input copy its last call read (its buffers hold that copy's result);
+        # copy -> timed steps that read it
+        self.lane_copy = lane_copy or {}
+        self.copy_steps = copy_steps or {}
 
 
 def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle=0.0):
@@ -526,10 +549,12 @@ def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle
     import torch
 
     n = len(lanes)
+    lane_copy = {}
 
     def call(k):
         lanes.detect_device(k, copies[k % len(copies)], cfg, bufs.out[k % n], bufs.offs[k % n],
                             after_current=False)
+        lane_copy[k % n] = k % len(copies)
 
     # the lanes do not wait on torch's stream: the inputs and buffers it just made must be done
     torch.cuda.synchronize()
@@ -572,7 +597,11 @@ def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle
         det.extend(d.tolist())
         com.extend(c.tolist())
         ctx.set_timing(False)
-    return Timed(elapsed, span_ms, det, com, (steps - 1) % n, steps, n)
+    copy_steps = {}
+    for k in range(steps):
+        copy_steps[k % len(copies)] = copy_steps.get(k % len(copies), 0) + 1
+    return Timed(elapsed, span_ms, det, com, (steps - 1) % n, steps, n, dict(lane_copy),
+                 copy_steps)
 
 
 def roofline_of(t, alg_bytes, in_bytes, traffic):
@@ -610,21 +639,69 @@ def roofline_of(t, alg_bytes, in_bytes, traffic):
             "measured_achievable_peak": 6290.0}
 
 
-def check_parity(oracle, frames, pts, offsets, first, count, t, n, nms, W):
-    """Sampled frames against the CPU oracle, raster order inside every frame."""
-    ok = True
-    checked = []
-    for f in sorted({0, count // 2, count - 1}):
-        want = oracle.detect(frames[f].cpu().numpy(), t, n, nms)
-        ok &= bool(np.array_equal(pts[offsets[f]:offsets[f + 1]], want))
-        checked.append(first + f)
-    order_ok = True
-    for f in range(count):   # raster order inside every frame (size-independent property)
-        seg = pts[offsets[f]:offsets[f + 1]].astype(np.int64)
-        if len(seg) > 1:
-            key = seg[:, 1] * W + seg[:, 0]
-            order_ok &= bool(np.all(np.diff(key) > 0))
-    return {"oracle_frames": checked, "bit_exact": ok, "raster_order": order_ok}
+def raster_order_ok(pts, offsets, W):
+    """Keypoints strictly increasing in raster order inside every frame."""
+    if len(pts) < 2:
+        return True
+    key = pts[:, 1].astype(np.int64) * W + pts[:, 0].astype(np.int64)
+    inc = np.diff(key) > 0
+    # a frame boundary may step back: position offsets[f] - 1 -> offsets[f]
+    starts = np.asarray(offsets[1:-1], dtype=np.int64) - 1
+    starts = starts[(starts >= 0) & (starts < len(inc))]
+    inc[starts] = True
+    return bool(np.all(inc))
+
+
+def batch_parity(oracle, copies, bufs, tm, t, n, nms, W):
+    """Whole-batch parity outside the timed region (the reference's
+    integration test compares the whole output Vec, tests/compare.rs:45-61): every frame of
+    every input copy goes through the CPU checker (oracle.avx2_detect_batch: the AVX2 port of
+    src/fast_simd.rs over a thread pool, itself pinned to the scalar oracle by
+    tests/test_oracle.py), and every lane's last result -- offsets and points of all its
+    frames -- must equal its copy's.  The scalar oracle (oracle/fast_oracle.c) also checks the
+    first, middle and last frame of the last lane's copy directly.  Returns the record and the
+    keypoints per timed step (the copies' exact totals weighted by the steps that read them)."""
+    ref = {}
+    for c in range(len(copies)):
+        ref[c] = oracle.avx2_detect_batch(copies[c], t, n, nms)
+    count = copies[0].shape[0]
+    ok, order_ok, compared = True, True, []
+    for lane, c in sorted(tm.lane_copy.items()):
+        o = bufs.offs[lane][: count + 1].cpu().numpy().astype(np.uint64)
+        total = int(o[-1])
+        rp, ro = ref[c]
+        if total > bufs.out[lane].shape[0]:
+            ok = False
+            continue
+        p = bufs.out[lane][:total].cpu().numpy().astype(np.uint32)
+        ok &= bool(np.array_equal(o, ro)) and bool(np.array_equal(p, rp))
+        order_ok &= raster_order_ok(p, o, W)
+        compared.append({"lane": lane, "copy": c, "frames": count, "keypoints": total})
+    c_last = tm.lane_copy.get(tm.last, 0)
+    rp, ro = ref[c_last]
+    sampled = sorted({0, count // 2, count - 1})
+    scalar_ok = all(bool(np.array_equal(rp[ro[f]:ro[f + 1]],
+                                         oracle.detect(copies[c_last][f].cpu().numpy(), t, n, nms)))
+                    for f in sampled)
+    kp_per_copy = [int(ref[c][1][-1]) for c in range(len(copies))]
+    steps = sum(tm.copy_steps.values()) or 1
+    kp_step = sum(kp_per_copy[c] * s for c, s in tm.copy_steps.items()) / steps
+    rec = {"oracle_frames": "all", "frames_per_copy": count, "copies_checked": len(copies),
+           "lanes_compared": compared, "bit_exact": bool(ok and scalar_ok),
+           "gpu_equals_checker_all_frames": bool(ok), "raster_order": order_ok,
+           "checker": "oracle.avx2_detect_batch (AVX2 port, pinned to fast_oracle.c)",
+           "scalar_oracle_frames": sampled, "scalar_oracle_copy": c_last,
+           "scalar_oracle_equal": bool(scalar_ok), "keypoints_per_copy": kp_per_copy}
+    return rec, kp_step
+
+
+def select_device(ranks_share_device, world, local):
+    """(GPU index, process-group backend or None) of this rank: one process per GPU, rank
+    with LOCAL_RANK r on cuda:r over the default backend ("nccl" = RCCL on ROCm); with
+    --ranks-share-device every rank on cuda:0 over gloo (RCCL wants one rank per device)."""
+    if ranks_share_device:
+        return 0, ("gloo" if world > 1 else None)
+    return local, ("nccl" if world > 1 else None)
 
 
 def main(argv=None):
@@ -632,18 +709,18 @@ def main(argv=None):
     world, rank, local = dist_env()
     import torch
 
-    gpu = 0 if args.ranks_share_device else local
+    gpu, backend = select_device(args.ranks_share_device, world, local)
     if world > 1:
         import torch.distributed as dist
 
         global _REDUCE_DEVICE
-        if args.ranks_share_device:
+        if backend == "gloo":
             # several ranks on one GPU: RCCL wants one rank per device, so the barrier and
             # the reductions go over gloo on host tensors (the data path has no collective)
             dist.init_process_group(backend="gloo")
             _REDUCE_DEVICE = "cpu"
         else:
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group(backend=backend, device_id=torch.device("cuda", gpu))
     torch.cuda.set_device(gpu)
     device = torch.device("cuda", gpu)
 
@@ -659,9 +736,11 @@ def main(argv=None):
         first, count = strong_shard(rank, world, args.frames_total)
     else:
         first, count = shard_frames(rank, args.frames)
-    # a shard below 512 MiB is rotated through copies (>= 512 MiB in all), so that its frames come
-    # from HBM, not the 256 MiB Infinity Cache
-    copies = make_batch(workloads, first, count, W, H, device, min_bytes=1 << 29)
+    # one distinct copy of the shard per lane at least (no two launches in flight read the
+    # same bytes), and >= 512 MiB in all, so that its frames come from HBM, not the 256 MiB
+    # Infinity Cache
+    copies = make_batch(workloads, first, count, W, H, device, min_bytes=1 << 29,
+                        lanes=args.lanes)
     frames = copies[0]
     cap = max(count, 1) * 200_000
     stream = torch.cuda.current_stream(device)
@@ -674,17 +753,21 @@ def main(argv=None):
     tm = timed_steps(fast_hip, lanes, bufs, copies, cfg, args.steps, args.warmup, world,
                      settle=args.settle_seconds)
     elapsed = reduce_max(tm.elapsed, world, device)
-    total_kp = int(bufs.offs[tm.last][-1].item())
-    offsets = bufs.offs[tm.last].cpu().numpy()
 
-    # ---- parity of sampled frames against the CPU oracle (outside the timed region)
+    # ---- whole-batch parity against the CPU checker (outside the timed region), on every
+    # rank for its own shard, all-reduced
     parity = {}
-    if not args.no_extras:
-        pts = bufs.out[tm.last][: min(total_kp, cap)].cpu().numpy().astype(np.uint32)
-        parity = check_parity(oracle, frames, pts, offsets, first, count, args.threshold,
-                              args.count, nms, W)
-        parity["lanes_identical"] = all(
-            bool(torch.equal(bufs.offs[i], bufs.offs[tm.last])) for i in range(len(lanes)))
+    if args.no_parity:
+        kp_step = float(np.mean([int(bufs.offs[i][count].item()) for i in tm.lane_copy]))
+    else:
+        parity, kp_step = batch_parity(oracle, copies, bufs, tm, args.threshold, args.count,
+                                       nms, W)
+        bad = reduce_sum(0.0 if parity["bit_exact"] else 1.0, world, device)
+        parity["ranks"] = {"world": world, "ranks_bit_exact": int(world - bad),
+                           "all_ranks_bit_exact": bad == 0,
+                           "frames_checked_all_ranks": int(reduce_sum(
+                               float(count * len(parity["lanes_compared"])), world, device))}
+    total_kp = int(round(kp_step))
 
     frames_total = reduce_sum(float(count), world, device)
     kp_total = reduce_sum(float(total_kp), world, device)
@@ -713,17 +796,16 @@ def main(argv=None):
             t2 = timed_steps(fast_hip, lanes, bufs, copies, ocfg, args.steps, args.warmup,
                              world, settle=args.settle_seconds)
             e2 = reduce_max(t2.elapsed, world, device)
-            kp2 = int(bufs.offs[t2.last][-1].item())
-            pts2 = bufs.out[t2.last][: min(kp2, cap)].cpu().numpy().astype(np.uint32)
+            par2, kp2f = batch_parity(oracle, copies, bufs, t2, args.threshold, args.count,
+                                      NMS_NAMES[other], W)
+            kp2 = int(round(kp2f))
             leg = {"workload": f"same batch, nms={other}",
                    "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
                    "ms_per_step": round(e2 * 1e3 / args.steps, 4),
                    "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
                    "roofline": roofline_of(t2, in_bytes + 8 * kp2 + 4 * count, in_bytes,
                                            load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
-                   "parity": check_parity(oracle, frames, pts2, bufs.offs[t2.last].cpu().numpy(),
-                                          first, count, args.threshold, args.count,
-                                          NMS_NAMES[other], W)}
+                   "parity": par2}
             extras[f"nms_{other}"] = leg
         # the same batch on one lane (one stream: every launch waits for the previous call's
         # compaction): the protocol of rounds 1-3, and the isolated kernel's own duration
@@ -733,33 +815,38 @@ def main(argv=None):
         t1 = timed_steps(fast_hip, lanes1, buf1, copies, cfg, args.steps, args.warmup, world,
                          settle=args.settle_seconds)
         e1 = reduce_max(t1.elapsed, world, device)
-        kp1 = int(bufs.offs[0][-1].item())
+        kp1 = int(bufs.offs[0][count].item())
+        want1 = parity.get("keypoints_per_copy", [None] * len(copies))[t1.lane_copy.get(0, 0)]
         extras["single_lane"] = {
-            "workload": "same batch and config, one lane (one stream)",
+            "workload": "same batch and config, one lane (one stream), the same copies",
             "value": round(pixels / e1 * args.steps / 1e6, 1), "unit": "Mpixels/s",
             "ms_per_step": round(e1 * 1e3 / args.steps, 4),
-            "keypoints_equal": kp1 == total_kp,
-            "roofline": roofline_of(t1, in_bytes + 8 * kp1 + 4 * count, in_bytes,
+            "keypoints_equal": want1 is None or kp1 == want1,
+            "roofline": roofline_of(t1, in_bytes + 8 * total_kp + 4 * count, in_bytes,
                                     load_traffic(cfg_key))}
     if world > 1 and not strong and not args.no_strong_leg:
         # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU (run
         # with --no-extras too: it is the multi-GPU line's own strong-scaling number)
         f4, c4 = strong_shard(rank, world, 512)
-        cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29)
+        cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29, lanes=args.lanes)
         buf4 = LaneBufs(len(lanes), max(c4, 1) * 200_000, c4, device)
         t4 = timed_steps(fast_hip, lanes, buf4, cop4, cfg, args.steps, args.warmup, world,
                          settle=args.settle_seconds)
         e4 = reduce_max(t4.elapsed, world, device)
-        kp4 = int(reduce_sum(float(buf4.offs[t4.last][-1].item()), world, device))
+        par4, kp4f = batch_parity(oracle, cop4, buf4, t4, args.threshold, args.count, nms, W)
+        kp4 = int(reduce_sum(float(round(kp4f)), world, device))
+        bad4 = reduce_sum(0.0 if par4["bit_exact"] else 1.0, world, device)
         extras["config4_strong"] = {
             "workload": f"512 {W}x{H} frames in total, {c4} per GPU (rank {rank}), "
-                        f"nms={args.nms}; rotated through {len(cop4)} copies (HBM reads)",
+                        f"nms={args.nms}; rotated through {len(cop4)} distinct copies (HBM reads)",
             "value": round(512 * W * H / e4 * args.steps / 1e6, 1), "unit": "Mpixels/s",
             "ms_per_step": round(e4 * 1e3 / args.steps, 4), "scaling": "strong",
             "frames_total": 512, "keypoints_per_step": kp4,
             "lanes": t4.lanes,
             "kernel_ms_avg": round(t4.span_ms / t4.steps, 4),
-            "launch_ms_avg": round(float(np.mean(t4.det)), 4) if len(t4.det) else None}
+            "launch_ms_avg": round(float(np.mean(t4.det)), 4) if len(t4.det) else None,
+            "parity": {"oracle_frames": "all", "all_ranks_bit_exact": bad4 == 0,
+                       "rank0": par4}}
         del cop4, buf4
     if rank == 0 and not args.no_extras:
         # single-frame latency (device-resident frame, one launch, HIP events), on --input
@@ -796,7 +883,7 @@ def main(argv=None):
             fast_hip, _native, host,
             {"off": (cfg, 0), "maxt": (cfg, 1)})
         extras["config5_4k"] = config5_4k(fast_hip, Config, NonMaximalSuppression, workloads,
-                                          lanes, device, oracle.detect,
+                                          lanes, device,
                                           settle=args.settle_seconds)
         extras["rgb_path"] = rgb_path(fast_hip, cfg, frames, out, offs, stream)
         if world == 1 and args.cpu_seconds > 0:
@@ -818,7 +905,7 @@ def main(argv=None):
             "settle_seconds": args.settle_seconds,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic S1 (committed 300x200 golden fixture tiled, rolled per frame)",
+            "data": "synthetic S1 (committed 300x200 golden fixture tiled, rolled per frame; one distinct copy of the batch per lane)",
             "config": {"workload": f"{work}, t={args.threshold} n={args.count} nms={args.nms}",
                        "frames_per_gpu": count, "width": W, "height": H,
                        "threshold": args.threshold, "count": args.count, "nms": args.nms,

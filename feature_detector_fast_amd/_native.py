@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
     "fdf_detect_device_rgb", "fdf_circle", "fdf_calculate_offsets", "fdf_score_rings",
     "fdf_score_rings_device", "fdf_ctx_set_band_rows", "fdf_ctx_set_upload_chunks",
+    "fdf_ctx_recoveries",
 )
 
 
@@ -165,6 +166,8 @@ def load():
     lib.fdf_ctx_set_band_rows.argtypes = [vp, u32]
     lib.fdf_ctx_set_upload_chunks.restype = ctypes.c_int
     lib.fdf_ctx_set_upload_chunks.argtypes = [vp, u32]
+    lib.fdf_ctx_recoveries.restype = ctypes.c_int
+    lib.fdf_ctx_recoveries.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.fdf_ctx_timing_samples.restype = ctypes.c_int
     lib.fdf_ctx_timing_samples.argtypes = [vp, vp, vp, u32, ctypes.POINTER(u32)]
     lib.fdf_fetch_last.restype = ctypes.c_int
@@ -248,6 +251,13 @@ class Context:
         """fdf_detect's overlapped upload (fdf_ctx_set_upload_chunks): the frame in
         ``chunks`` row chunks while the detector runs; 1 = one copy first; 0 = default."""
         check(self._lib.fdf_ctx_set_upload_chunks(self.handle, int(chunks)))
+
+    def recoveries(self):
+        """(upload_fallbacks, lookback_recoveries) the host calls made on their own
+        (fdf_ctx_recoveries): both 0 in a healthy run."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._lib.fdf_ctx_recoveries(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def close(self):
         if self.handle:

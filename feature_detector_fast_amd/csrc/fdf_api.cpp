@@ -60,6 +60,13 @@ struct fdf_ctx {
     uint32_t* d_flags = nullptr;        // device: the chunk flags the bands poll
     uint32_t chunk_epoch = 0;
     uint32_t chunks = 0;                // upload chunks (0: kChunksDefault; 1: no overlap)
+    // recoveries the host entry points made on their own (fdf_ctx_recoveries): a band's wait
+    // for its upload chunk ran out and the frame was detected again from one copy; a
+    // direct-output look-back ran out and the compaction rebuilt the output from the slots
+    uint64_t upload_fallbacks = 0, lookback_recoveries = 0;
+    // an asynchronous device call's look-back ran out and a host call found the error word
+    // first: kept here and returned by the next fdf_detect_device(_rgb), as fdf.h promises
+    bool pending_device_error = false;
     uint16_t* d_scores = nullptr;       size_t scores_n = 0;       // host-API scores
     uint8_t* d_slots = nullptr;         size_t slots_bytes = 0;    // per-band output slots
     uint32_t* d_counts = nullptr;       size_t counts_n = 0;       // per-band keypoint counts
@@ -658,6 +665,9 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     // the host frames are read by the copies below: nothing else may still read d_in (nor
     // the host output, which the host reads after this call)
     wait_done(ctx);
+    // an error an earlier asynchronous fdf_detect_device left in the error word belongs to
+    // that call: keep it for the next device call, so this call's own check sees only its own
+    if (take_lookback_error(ctx)) ctx->pending_device_error = true;
     // one grey frame of >= kChunkMinBytes: upload it in row chunks on the copy stream while
     // the detector runs, each band waiting for the chunk of its last row (the H2D of a 1080p
     // frame is ~45 us, the detector ~20 us: DESIGN.md §7.5)
@@ -665,8 +675,12 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
 #ifdef FDF_DEBUG_BUILD   // A/B of the overlapped upload (tools/host_latency.py): FDF_CHUNKS=1 disables it
     if (const char* e = std::getenv("FDF_CHUNKS")) ctx->chunks = (uint32_t)std::strtoul(e, nullptr, 0);
 #endif
+    // (the chunk count in effect must be > 1: one chunk is one copy before the launch, which
+    // the plain path below does without the flag copy and the second stream)
+    const uint32_t nchunks_eff = std::min<uint32_t>(ctx->chunks ? ctx->chunks : kChunksDefault,
+                                                    kMaxChunks);
     const bool chunked = host_out && !rgb && n_frames == 1 && frame_bytes >= kChunkMinBytes &&
-                         ctx->chunks != 1 && ctx->h_stats && ensure_chunk_flags(ctx) == FDF_OK;
+                         nchunks_eff > 1 && ctx->h_stats && ensure_chunk_flags(ctx) == FDF_OK;
     // one packed grey frame in pinned (page-locked, non-coherent) host memory, unscored: the
     // detector reads it in place over PCIe, with no copy before the launch -- its row stream
     // is the upload (1080p max-t 72-75 vs 82-83 us end to end).  Host writes
@@ -677,20 +691,30 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     // fdf_fetch_last (detect_host).
     const uint8_t* in_place = nullptr;
     if (ctx->chunks == 0 && host_out && !rgb && n_frames == 1 && row_stride == w) {
-        hipPointerAttribute_t a;
+        // the frame's first and last bytes must both be pinned and map to one contiguous
+        // device range: a hipHostRegister'ed sub-range shorter than the frame is copied, not
+        // read past its end
+        hipPointerAttribute_t a, z;
         if (hipPointerGetAttributes(&a, data) == hipSuccess) {
             if (a.type == hipMemoryTypeHost && a.devicePointer &&
-                !(a.allocationFlags & hipHostMallocCoherent))
-                in_place = static_cast<const uint8_t*>(a.devicePointer);
+                !(a.allocationFlags & hipHostMallocCoherent)) {
+                const uint8_t* last = data + frame_bytes - 1;
+                if (hipPointerGetAttributes(&z, last) == hipSuccess) {
+                    if (z.type == hipMemoryTypeHost && z.devicePointer &&
+                        static_cast<const uint8_t*>(z.devicePointer) ==
+                            static_cast<const uint8_t*>(a.devicePointer) + (frame_bytes - 1))
+                        in_place = static_cast<const uint8_t*>(a.devicePointer);
+                } else {
+                    (void)hipGetLastError();   // the frame runs past the pinned range
+                }
+            }
         } else {
             (void)hipGetLastError();   // pageable memory: not an error here
         }
     }
     if (in_place) {
     } else if (chunked) {
-        const uint32_t nchunks = std::min<uint32_t>(ctx->chunks ? ctx->chunks : kChunksDefault,
-                                                    kMaxChunks);
-        up.rows = (h + nchunks - 1) / nchunks;
+        up.rows = (h + nchunks_eff - 1) / nchunks_eff;
         up.epoch = ++ctx->chunk_epoch == 0 ? ++ctx->chunk_epoch : ctx->chunk_epoch;
         up.flags = ctx->d_flags;
         for (uint32_t r0 = 0, c = 0; r0 < h; r0 += up.rows, ++c) {
@@ -760,6 +784,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         if (err & 2u) {
             // a band's wait for its upload chunk ran out (the copies are drained now): detect
             // again from the whole frame, uploaded before the launch
+            ++ctx->upload_fallbacks;
             const uint32_t saved = ctx->chunks;
             ctx->chunks = 1;
             rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs,
@@ -770,6 +795,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         // a direct-output band's look-back ran out (band_lookback): the offsets and points of
         // its frame on are not written; the slots and counts are, so the compaction rebuilds
         // both from them
+        ++ctx->lookback_recoveries;
         fdfk::CompactParams c = ctx->last_compact;
         c.kp_stats = nullptr;
         c.group_sums = nullptr;
@@ -1023,6 +1049,14 @@ int fdf_ctx_workspace_bytes(fdf_ctx* ctx, uint64_t* bytes) {
     return FDF_OK;
 }
 
+int fdf_ctx_recoveries(fdf_ctx* ctx, uint64_t* upload_fallbacks, uint64_t* lookback_recoveries) {
+    if (!ctx) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (upload_fallbacks) *upload_fallbacks = ctx->upload_fallbacks;
+    if (lookback_recoveries) *lookback_recoveries = ctx->lookback_recoveries;
+    return FDF_OK;
+}
+
 int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
     if (!ctx) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);
@@ -1189,7 +1223,11 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
     DeviceGuard guard(ctx->device);
     // an earlier asynchronous direct-output launch of this context had a look-back wait run
     // out (band_lookback; never seen in practice): its output was incomplete -- reported once
-    if (take_lookback_error(ctx)) return FDF_ERR_DEVICE;
+    // (also when a host call in between found the error word first: pending_device_error)
+    if (take_lookback_error(ctx) || ctx->pending_device_error) {
+        ctx->pending_device_error = false;
+        return FDF_ERR_DEVICE;
+    }
     if (empty) {
         return hipMemsetAsync(d_frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull), s) ==
                        hipSuccess
@@ -1221,7 +1259,11 @@ int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_fram
     DeviceGuard guard(ctx->device);
     // an earlier asynchronous direct-output launch of this context had a look-back wait run
     // out (band_lookback; never seen in practice): its output was incomplete -- reported once
-    if (take_lookback_error(ctx)) return FDF_ERR_DEVICE;
+    // (also when a host call in between found the error word first: pending_device_error)
+    if (take_lookback_error(ctx) || ctx->pending_device_error) {
+        ctx->pending_device_error = false;
+        return FDF_ERR_DEVICE;
+    }
     if (empty) {
         return hipMemsetAsync(d_frame_offsets, 0, sizeof(uint64_t) * (n_frames + 1ull), s) ==
                        hipSuccess

@@ -302,7 +302,13 @@ class Lanes:
         return self._ext[lane]
 
     def detect_device(self, k, frames, config, out, offsets, after_current=True):
-        """detect_device on lane k % n (asynchronous on that lane's stream)."""
+        """detect_device on lane k % n (asynchronous on that lane's stream).
+
+        The call borrows ``frames``, ``out`` and ``offsets`` until the lane's work is done,
+        as the reference's detector borrows its image for the call (src/fast_simd.rs:847):
+        each is recorded on the lane's stream (``Tensor.record_stream``), so torch's caching
+        allocator does not hand their memory to another tensor while the lane still reads or
+        writes it, even when the caller drops its last reference right after this call."""
         import torch
 
         lane = k % len(self.ctxs)
@@ -311,6 +317,8 @@ class Lanes:
             s.wait_stream(torch.cuda.current_stream(frames.device))
         detect_device(frames, config, out, offsets, stream=s, device=self.device,
                       ctx=self.ctxs[lane])
+        for t in (frames, out, offsets):
+            t.record_stream(s)
         return lane
 
     def wait(self, lane=None):

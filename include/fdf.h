@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FDF_ABI_VERSION 5
+#define FDF_ABI_VERSION 6
 
 /* Status codes.  Shapes the reference maps to an empty Vec return FDF_OK with 0 points. */
 enum fdf_status {
@@ -130,6 +130,15 @@ int fdf_ctx_set_upload_chunks(fdf_ctx* ctx, uint32_t chunks);
  * slots and counts, compaction sums).  Slots take 1/8 byte per pixel of the largest batch
  * seen; nothing in the workspace scales with more than that. */
 int fdf_ctx_workspace_bytes(fdf_ctx* ctx, uint64_t* bytes);
+
+/* Recoveries the host entry points made on their own since the context was created (ABI 6;
+ * either pointer may be NULL): `upload_fallbacks` counts fdf_detect calls whose overlapped
+ * upload (fdf_ctx_set_upload_chunks k > 1) had a band's chunk wait run out, so the frame was
+ * detected again from one copy; `lookback_recoveries` counts host calls whose direct-output
+ * look-back ran out and whose output the compaction rebuilt from the band slots.  Both stay
+ * 0 in a healthy run -- tests assert it, so a handshake that never works cannot pass by its
+ * fallback. */
+int fdf_ctx_recoveries(fdf_ctx* ctx, uint64_t* upload_fallbacks, uint64_t* lookback_recoveries);
 
 /*
  * Replaces fast_simd::detector(img, config) -> Vec<Point> (src/fast_simd.rs:847).

@@ -303,6 +303,46 @@ double fdf_avx2_time_pinned(const uint8_t* frames, uint32_t n_frames, size_t fra
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// Whole-batch checker: the keypoints of every frame (frame f at frames + f * frame_stride,
+// the batch padded as above), frame f on worker f % threads, concatenated in frame order.
+// offsets[f] .. offsets[f+1] are frame f's points; the first `cap` points go to out_xy.
+// Returns the total, or a negative error as fdf_avx2_detect.
+int64_t fdf_avx2_detect_batch(const uint8_t* frames, uint32_t n_frames, size_t frame_stride,
+                              uint32_t w, uint32_t h, uint8_t t, uint8_t n, uint8_t nms,
+                              int threads, uint32_t* out_xy, size_t cap, uint64_t* offsets) {
+    if (n < 9 || n > 16) return -1;
+    if (nms > 2) return -4;
+    if (h < 3 || (h > 6 && w < 6)) return -2;
+    if (threads < 1) threads = 1;
+    std::vector<std::vector<Pt>> per(n_frames);
+    auto worker = [&](int tid) {
+        for (uint32_t f = tid; f < n_frames; f += threads) {
+            if (h <= 6 || w == 6) continue;
+            const uint8_t* d = frames + (size_t)f * frame_stride;
+            if (nms == kOff) detect<kOff>(d, w, h, t, n, per[f]);
+            else if (nms == kMaxT) detect<kMaxT>(d, w, h, t, n, per[f]);
+            else detect<kSad>(d, w, h, t, n, per[f]);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < threads; ++i) pool.emplace_back(worker, i);
+    worker(0);
+    for (auto& th : pool) th.join();
+    uint64_t k = 0;
+    for (uint32_t f = 0; f < n_frames; ++f) {
+        if (offsets) offsets[f] = k;
+        for (const Pt& p : per[f]) {
+            if (k < cap) {
+                out_xy[2 * k] = p.x;
+                out_xy[2 * k + 1] = p.y;
+            }
+            ++k;
+        }
+    }
+    if (offsets) offsets[n_frames] = k;
+    return (int64_t)k;
+}
+
 double fdf_avx2_time(const uint8_t* frames, uint32_t n_frames, size_t frame_stride,
                      uint32_t w, uint32_t h, uint8_t t, uint8_t n, uint8_t nms, int threads,
                      int reps, uint64_t* total) {

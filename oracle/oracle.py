@@ -78,6 +78,10 @@ def _load_avx2():
         lib.fdf_avx2_time_pinned.argtypes = [ctypes.c_void_p, u32, ctypes.c_size_t, u32, u32, u8,
                                              u8, u8, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                              ctypes.POINTER(ctypes.c_uint64)]
+        lib.fdf_avx2_detect_batch.restype = ctypes.c_int64
+        lib.fdf_avx2_detect_batch.argtypes = [ctypes.c_void_p, u32, ctypes.c_size_t, u32, u32, u8,
+                                              u8, u8, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_void_p]
         lib.fdf_avx2_samples.restype = ctypes.c_int64
         lib.fdf_avx2_samples.argtypes = [ctypes.c_void_p, u32, u32, u8, u8, u8, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_void_p]
@@ -185,6 +189,54 @@ def avx2_detect(img, t, n, nms):
     if cnt:
         lib.fdf_avx2_detect(buf.ctypes.data, w, h, t, n, int(nms), out.ctypes.data, cnt)
     return out
+
+
+def checker_threads():
+    """Worker threads for whole-batch checks: the CPUs this process may use, at most the
+    cgroup quota and at most 16 (the GPU box's CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(16, n))
+
+
+def avx2_detect_batch(frames, t, n, nms, threads=None):
+    """Every frame of a (F, H, W) stack (numpy, or a torch tensor on any device) through the
+    AVX2 port (pinned to the scalar oracle: tests/test_oracle.py), frame f on worker
+    f % threads.  Returns (points (K, 2) uint32, offsets (F+1,) uint64) in frame order -- the
+    layout of fdf_detect_batch / detect_device -- for whole-batch parity checks."""
+    if hasattr(frames, "cpu"):
+        frames = frames.cpu().numpy()
+    frames = np.asarray(frames, dtype=np.uint8)
+    if frames.ndim != 3:
+        raise ValueError("(F, H, W) stack expected")
+    f, h, w = frames.shape
+    buf = np.zeros(frames.size + 16, dtype=np.uint8)
+    buf[: frames.size] = frames.reshape(-1)
+    lib = _load_avx2()
+    offsets = np.zeros(f + 1, dtype=np.uint64)
+    th = checker_threads() if threads is None else int(threads)
+    # one keypoint per 32 pixels first (real images: ~1 per 100); a denser batch runs again
+    # with the exact size
+    cap = max(1024, frames.size // 32)
+    out = np.empty((cap, 2), dtype=np.uint32)
+    cnt = lib.fdf_avx2_detect_batch(buf.ctypes.data, f, h * w, w, h, t, n, int(nms), th,
+                                    out.ctypes.data, cap, offsets.ctypes.data)
+    if cnt < 0:
+        raise OracleError(cnt)
+    if cnt > cap:
+        out = np.empty((cnt, 2), dtype=np.uint32)
+        lib.fdf_avx2_detect_batch(buf.ctypes.data, f, h * w, w, h, t, n, int(nms), th,
+                                  out.ctypes.data, cnt, offsets.ctypes.data)
+    return out[:cnt], offsets
 
 
 def avx2_time(frames, t, n, nms, threads=1, reps=1, cpus=None):

@@ -30,7 +30,7 @@ def test_header_symbols_are_exported():
 
 def test_abi_version_and_status_strings():
     lib = _native.load()
-    assert lib.fdf_abi_version() == 5
+    assert lib.fdf_abi_version() == 6
     for code in range(8):
         assert lib.fdf_status_string(code)
     assert _native.status_string(_native.FDF_ERR_COUNT).startswith("count")

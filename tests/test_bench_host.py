@@ -18,6 +18,52 @@ def test_timing_every(steps, every):
     assert steps // every >= min(steps, bench.MIN_TIMED)
 
 
+@pytest.mark.parametrize("local", [0, 1, 5, 7])
+def test_select_device_one_rank_per_gpu(local):
+    """The driver's torchrun path: LOCAL_RANK r -> cuda:r over the default backend (RCCL);
+    --ranks-share-device -> every rank on cuda:0 over gloo."""
+    assert bench.select_device(False, 8, local) == (local, "nccl")
+    assert bench.select_device(True, 8, local) == (0, "gloo")
+    assert bench.select_device(False, 1, 0) == (0, None)
+    args = bench.parse_args(["--gpus", "8"])
+    assert not args.ranks_share_device and args.lanes == 3
+
+
+@pytest.mark.parametrize("batch,lanes,need,copies", [
+    (512 * 1920 * 1080, 3, 1 << 29, 3),      # headline: one 1.06 GB copy per lane
+    (64 * 1920 * 1080, 3, 1 << 29, 6),       # 8-GPU strong shard: >= 512 MiB, lanes multiple
+    (128 * 3840 * 2160, 3, 0, 3),            # config 5
+    (10, 1, 0, 1), (10, 2, 25, 4)])
+def test_copies_per_lane(batch, lanes, need, copies):
+    """At least one distinct input copy per lane (no two launches in flight read the same
+    bytes), >= min_bytes in all, a multiple of the lanes."""
+    n = bench.n_copies(batch, lanes, need)
+    assert n == copies and n % lanes == 0 and n * batch >= need
+
+
+def test_copies_differ_and_lanes_keep_their_copies():
+    import numpy as np
+
+    import workloads
+    # copy c's frame k is S1 frame first + k + 211 c: a different roll at every position
+    for k in range(0, 600, 7):
+        for c in (1, 2, 3, 4, 5):
+            assert workloads.s1_roll(k) != workloads.s1_roll(k + bench.COPY_ROLL * c)
+    # step k on lane k % L reads copy k % C, C a multiple of L: a lane keeps to its copies
+    L, C = 3, bench.n_copies(64, 3, 200)
+    for k in range(50):
+        assert (k % C) % L == k % L
+    assert np.unique([(k % C) for k in range(50) if k % L == 1]).tolist() == [1, 4]
+
+
+def test_raster_order_check():
+    import numpy as np
+    pts = np.array([[5, 3], [9, 3], [4, 4], [3, 3], [8, 3]], dtype=np.uint32)
+    assert bench.raster_order_ok(pts, [0, 3, 5], 100)          # frame boundary at 3
+    assert not bench.raster_order_ok(pts, [0, 5], 100)
+    assert bench.raster_order_ok(pts[:0], [0, 0], 100)
+
+
 def test_roofline_from_timed_region():
     W, H, F, K = 1920, 1080, 512, 2_000_000
     in_bytes = F * W * H

@@ -73,13 +73,13 @@ def test_band_rows_4k(rows, nms):
 
 
 def test_config5_batch_repeated():
-    """BASELINE config 5's shape on one GPU: a 32-frame 4K t=8 n=12 SAD batch, launched 3
+    """BASELINE config 5's shape on one GPU: the bench's 128-frame 4K t=8 n=12 SAD batch, launched 3
     times (the band height follows the first launch's measured density from launch 2 on).
-    All three launches give the same lists, and frame 0 plus the three densest frames
-    equal the oracle."""
+    All three launches give the same lists, every frame equals the CPU checker, and frame 0
+    plus the three densest frames equal the scalar oracle."""
     import torch
 
-    F, W, H = 32, 3840, 2160
+    F, W, H = 128, 3840, 2160
     batch = workloads.s1_frames_torch(0, F, W, H)
     cfg = Config(8, 12, NonMaximalSuppression.SumAbsolute)
     out = torch.empty((F * 120_000, 2), dtype=torch.int32, device="cuda")
@@ -110,6 +110,9 @@ def test_config5_batch_repeated():
     for f in sorted({0, *dens.tolist()}):
         want = oracle.detect(batch[f].cpu().numpy(), 8, 12, 2)
         assert np.array_equal(p[o[f]:o[f + 1]], want), f
+    # every frame: the CPU checker (AVX2 port, pinned to the scalar oracle)
+    ref_pts, ref_offs = oracle.avx2_detect_batch(batch, 8, 12, 2)
+    assert np.array_equal(o.astype(np.uint64), ref_offs) and np.array_equal(p, ref_pts)
 
 
 @pytest.mark.parametrize("nms", [0, 1, 2])

@@ -164,3 +164,30 @@ def test_in_place_other_pinned_kinds(kind):
             assert hip.hipHostFree(ptr) == 0
         else:
             assert hip.hipHostUnregister(ptr) == 0
+
+
+def test_in_place_registered_range_shorter_than_frame():
+    """a frame whose first bytes sit in a hipHostRegister'ed range that ends before
+    the frame does is copied, not read in place (reading it in place would read past the
+    registration over PCIe).  The frame's last byte must map to the same contiguous device
+    range as its first (fdf_api.cpp run_host)."""
+    W, H = 1280, 720
+    img = workloads.s1_frame(11, W, H)
+    hip = _hip()
+    keep = np.zeros(W * H + 4096, dtype=np.uint8)
+    base = keep.ctypes.data + (-keep.ctypes.data) % 4096
+    view = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
+    view[:] = img.reshape(-1)
+    half = (W * H // 2) & ~4095                       # whole pages, half the frame
+    assert hip.hipHostRegister(ctypes.c_void_p(base), ctypes.c_size_t(half), ctypes.c_uint(0)) == 0
+    lib = _native.load()
+    ctx = _native.Context(0)
+    try:
+        for nms in (0, 1, 2):
+            rc, got, _ = _detect(lib, ctx, base, W, H, 16, 9, nms)
+            _native.check(rc, "fdf_detect")
+            assert np.array_equal(got, oracle.detect(img, 16, 9, nms)), nms
+        assert ctx.recoveries() == (0, 0)
+    finally:
+        ctx.close()
+        assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0

@@ -1,0 +1,102 @@
+"""Stream-ordered lifetime of the tensors a launch lane borrows.
+
+The reference's detector borrows its image for the length of a synchronous call
+(src/fast_simd.rs:847-859).  fast_hip.Lanes enqueues the call on a lane's own HIP stream and
+returns at once, so the borrow has to last until that stream is done: Lanes.detect_device
+records ``frames``, ``out`` and ``offsets`` on the lane's stream (Tensor.record_stream), and
+torch's caching allocator then keeps their memory out of reuse until the lane's work is done.
+
+The test makes the hazard certain if the borrow is not honoured: every lane first waits behind
+a long spin kernel on a side stream, 30 calls are enqueued on freshly allocated batch tensors
+that are dropped right after the call, and between calls same-sized tensors are allocated and
+filled with 0xFF on torch's current stream (which is not blocked, so those fills run while the
+lanes still wait).  After lanes.wait() every result must equal the CPU oracle
+(oracle/fast_oracle.c, pinned to the reference's goldens).  The second test removes
+record_stream and shows that the same sequence then reads overwritten frames."""
+import numpy as np
+import pytest
+
+import workloads
+from feature_detector_fast_amd import Config, NonMaximalSuppression, fast_hip
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+W, H, NF = 640, 480, 6
+
+
+def _hosts():
+    gens = (workloads.s1_frame, workloads.s3_frame, workloads.s2_frame)
+    return [np.stack([gens[b](7 * b + i, W, H) for i in range(NF)]) for b in range(3)]
+
+
+def _block_lanes(torch, lanes):
+    """Every lane waits behind ~20 ms of spin kernel on a side stream."""
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(50_000_000)
+        else:   # a long chain of small matmuls
+            a = torch.randn(512, 512, device="cuda")
+            for _ in range(400):
+                a = a @ a
+                a = a / (a.abs().max() + 1)
+    for i in range(len(lanes)):
+        lanes.stream(i).wait_stream(side)
+    return side
+
+
+def _run(torch, hosts, cfg, calls=30):
+    lanes = fast_hip.Lanes(3)
+    try:
+        torch.cuda.synchronize()
+        side = _block_lanes(torch, lanes)
+        outs, offs = [], []
+        for k in range(calls):
+            frames = torch.from_numpy(hosts[k % 3]).cuda()       # fresh, on the current stream
+            out = torch.full((NF * 60_000, 2), -1, dtype=torch.int32, device="cuda")
+            off = torch.zeros(NF + 1, dtype=torch.int64, device="cuda")
+            lanes.detect_device(k, frames, cfg, out, off)
+            del frames                                             # the lane still needs it
+            junk = torch.empty((NF, H, W), dtype=torch.uint8, device="cuda")
+            junk.fill_(0xFF)                                       # runs now: not blocked
+            del junk
+            outs.append(out)
+            offs.append(off)
+        lanes.wait()
+        torch.cuda.synchronize()
+        del side
+        return [(o.cpu().numpy(), p.cpu().numpy()) for o, p in zip(offs, outs)]
+    finally:
+        lanes.close()
+
+
+@pytest.mark.parametrize("nms", [1, 0])
+def test_lanes_borrow_until_done(nms):
+    import torch
+
+    hosts = _hosts()
+    want = [[oracle.detect(h[f], 16, 9, nms) for f in range(NF)] for h in hosts]
+    cfg = Config(16, 9, NonMaximalSuppression(nms))
+    res = _run(torch, hosts, cfg)
+    for k, (o, p) in enumerate(res):
+        for f in range(NF):
+            got = p[o[f]:o[f + 1]].astype(np.uint32)
+            assert np.array_equal(got, want[k % 3][f]), (k, f, len(got), len(want[k % 3][f]))
+
+
+def test_without_record_stream_the_hazard_is_real(monkeypatch):
+    """The same sequence with Tensor.record_stream made a no-op: the lanes read frames whose
+    memory the allocator has handed to the 0xFF fills (the test above would then fail).
+    Skipped, not failed, if this allocator happens not to reuse the blocks."""
+    import torch
+
+    hosts = _hosts()
+    want = [[oracle.detect(h[f], 16, 9, 1) for f in range(NF)] for h in hosts]
+    monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None)
+    res = _run(torch, hosts, Config(16, 9, NonMaximalSuppression(1)))
+    bad = sum(not np.array_equal(p[o[f]:o[f + 1]].astype(np.uint32), want[k % 3][f])
+              for k, (o, p) in enumerate(res) for f in range(NF))
+    if bad == 0:
+        pytest.skip("the allocator reused no freed frame block in this run")
+    assert bad > 0

@@ -35,10 +35,16 @@ def launch_twice_and_check(frames, t, n, nms, n_check=2):
     assert torch.equal(out, first_pts), (t, n, nms)
     o = offs.cpu().numpy()
     counts = np.diff(o)
+    pts = out[:total].cpu().numpy().astype(np.uint32)
     for f in sorted({0, *np.argsort(counts)[-n_check:].tolist()}):
-        got = out[o[f]:o[f + 1]].cpu().numpy().astype(np.uint32)
         want = oracle.detect(frames[f].cpu().numpy(), t, n, nms)
-        assert np.array_equal(got, want), (f, t, n, nms, len(got), len(want))
+        assert np.array_equal(pts[o[f]:o[f + 1]], want), (f, t, n, nms, len(want))
+    # every frame of the batch: the CPU checker (the AVX2 port over a thread pool, pinned to
+    # the scalar oracle by tests/test_oracle.py), offsets and points of the whole output
+    # (the reference compares whole Vecs: tests/compare.rs:45-61)
+    ref_pts, ref_offs = oracle.avx2_detect_batch(frames, t, n, nms)
+    assert np.array_equal(o.astype(np.uint64), ref_offs), (t, n, nms)
+    assert np.array_equal(pts, ref_pts), (t, n, nms)
     return total
 
 
@@ -83,11 +89,13 @@ def test_mixed_batch_full_geometry(mixed_batch, t, n, nms):
         ctx.set_geometry(0)
 
 
-def test_config4_exact_batch(s1_batch):
+@pytest.mark.parametrize("nms", [1, 0, 2])
+def test_config4_exact_batch(s1_batch, nms):
     """BASELINE.json config 4's exact per-GPU workload: 512 S1 1080p frames, t=16 n=9,
-    max-t NMS -- launched twice (device-side equality), frame 0 and the 3 densest frames
-    against the oracle."""
-    launch_twice_and_check(s1_batch, 16, 9, 1, n_check=3)
+    max-t NMS (and the bench's NMS-off / SAD legs) -- launched twice (device-side
+    equality), every frame against the CPU checker, frame 0 and the 3 densest frames against
+    the scalar oracle."""
+    launch_twice_and_check(s1_batch, 16, 9, nms, n_check=3)
 
 
 @pytest.mark.parametrize("nms", [1, 2])

@@ -232,6 +232,9 @@ def test_host_overlapped_upload(chunks):
                     img = padded[:, : f.shape[1]]
                 got = fast_hip.detect_array(img, Config(16, 9, NonMaximalSuppression(nms)))
                 assert np.array_equal(got, want[(i, nms)]), (rep, i, nms)
+        # the flag handshake worked: no band's chunk wait ran out and fell back to a second
+        # detection from one copy, and no look-back was rebuilt
+        assert ctx.recoveries() == (0, 0), ctx.recoveries()
     finally:
         ctx.set_upload_chunks(0)
 

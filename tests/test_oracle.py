@@ -197,6 +197,22 @@ def test_avx2_port_matches_oracle(golden, nms):
                                   oracle.detect(img, t, n, nms)), (img.shape, t, n, nms)
 
 
+@pytest.mark.parametrize("nms", [0, 1, 2])
+def test_avx2_batch_checker_matches_oracle(nms):
+    """The whole-batch checker bench.py and the batch parity tests use (the AVX2 port over a
+    thread pool) equals the scalar oracle frame by frame, in frame order, on the bench's own
+    shapes: S1 1080p t=16 n=9 and S1 4K t=8 n=12 (configs 4 and 5), plus dense noise."""
+    cases = [(np.stack([workloads.s1_frame(i) for i in (0, 211, 422)]), 16, 9),
+             (np.stack([workloads.s3_frame(i, 300, 200) for i in range(5)]), 16, 9),
+             (workloads.s1_frame(5, 3840, 2160)[None], 8, 12)]
+    for frames, t, n in cases:
+        pts, offs = oracle.avx2_detect_batch(frames, t, n, nms, threads=3)
+        assert offs[0] == 0 and offs[-1] == len(pts)
+        for f in range(frames.shape[0]):
+            want = oracle.detect(frames[f], t, n, nms)
+            assert np.array_equal(pts[offs[f]:offs[f + 1]], want), (frames.shape, f, nms)
+
+
 # --- synthetic workload generators (SURVEY.md §8d counts) --------------------------------
 
 def test_s1_1080p_counts():
