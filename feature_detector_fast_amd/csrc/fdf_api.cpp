@@ -60,6 +60,10 @@ struct fdf_ctx {
     uint32_t* d_flags = nullptr;        // device: the chunk flags the bands poll
     uint32_t chunk_epoch = 0;
     uint32_t chunks = 0;                // upload chunks (0: kChunksDefault; 1: no overlap)
+    // host frames that start in pinned memory but run past its mapping (a hipHostRegister'ed
+    // range shorter than the frames) are packed into this pinned buffer by the CPU first: the
+    // runtime's DMA copy rejects such a source range
+    uint8_t* h_stage = nullptr;         uint8_t* hd_stage = nullptr;   size_t h_stage_bytes = 0;
     // recoveries the host entry points made on their own (fdf_ctx_recoveries): a band's wait
     // for its upload chunk ran out and the frame was detected again from one copy; a
     // direct-output look-back ran out and the compaction rebuilt the output from the slots
@@ -712,6 +716,38 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             (void)hipGetLastError();   // pageable memory: not an error here
         }
     }
+    // frames that start in pinned host memory must lie inside one pinned mapping for the DMA
+    // copies below; a range that runs past it is packed into the pinned staging buffer first
+    if (!in_place && !chunked) {
+        const size_t span = (size_t)(n_frames - 1) * frame_stride + (size_t)(h - 1) * row_stride +
+                            px * w;
+        hipPointerAttribute_t a, z;
+        if (hipPointerGetAttributes(&a, data) == hipSuccess) {
+            if (a.type == hipMemoryTypeHost && a.devicePointer) {
+                const bool inside =
+                    hipPointerGetAttributes(&z, data + span - 1) == hipSuccess &&
+                    z.type == hipMemoryTypeHost &&
+                    static_cast<const uint8_t*>(z.devicePointer) ==
+                        static_cast<const uint8_t*>(a.devicePointer) + (span - 1);
+                if (!inside) {
+                    (void)hipGetLastError();
+                    const size_t fb = px * frame_bytes;
+                    if ((rc = ensure_host(ctx, &ctx->h_stage, &ctx->hd_stage, &ctx->h_stage_bytes,
+                                          fb * n_frames, ctx->stream)))
+                        return rc;
+                    for (uint32_t f = 0; f < n_frames; ++f)
+                        for (uint32_t y = 0; y < h; ++y)
+                            std::memcpy(ctx->h_stage + f * fb + (size_t)y * px * w,
+                                        data + f * frame_stride + (size_t)y * row_stride, px * w);
+                    data = ctx->h_stage;
+                    row_stride = px * w;
+                    frame_stride = fb;
+                }
+            }
+        } else {
+            (void)hipGetLastError();   // pageable memory
+        }
+    }
     if (in_place) {
     } else if (chunked) {
         up.rows = (h + nchunks_eff - 1) / nchunks_eff;
@@ -1012,6 +1048,7 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         if (ctx->h_out) (void)hipHostFree(ctx->h_out);
         if (ctx->h_offs) (void)hipHostFree(ctx->h_offs);
         if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+        if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
         (void)hipFree(ctx->d_flags);
         if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
         (void)hipFree(ctx->d_scores);

@@ -4,6 +4,7 @@
 returns ``list[Point]`` in raster order.  Array and batched variants return numpy arrays;
 ``detect_device`` keeps everything in HBM (torch CUDA tensors) for throughput.
 """
+import collections
 import ctypes
 import threading
 
@@ -288,6 +289,8 @@ class Lanes:
             ctx.lock = threading.Lock()
             self.ctxs.append(ctx)
         self._ext = [None] * n
+        # per lane: (event recorded after a call, the tensors that call borrows), oldest first
+        self._held = [collections.deque() for _ in range(n)]
 
     def __len__(self):
         return len(self.ctxs)
@@ -301,14 +304,30 @@ class Lanes:
                                                         device=torch.device("cuda", self.device))
         return self._ext[lane]
 
+    def _hold(self, lane, tensors):
+        """Keep `tensors` referenced until the lane's stream has passed the call just enqueued
+        (an event recorded after it), and drop the references of earlier calls it has passed.
+        (Not Tensor.record_stream: the caching allocator would then record events on the lane's
+        stream when the tensor is freed, which may be after the context -- and its stream --
+        is gone.)"""
+        import torch
+
+        q = self._held[lane]
+        while q and q[0][0].query():
+            q.popleft()
+        ev = torch.cuda.Event()
+        ev.record(self.stream(lane))
+        q.append((ev, tensors))
+
     def detect_device(self, k, frames, config, out, offsets, after_current=True):
         """detect_device on lane k % n (asynchronous on that lane's stream).
 
         The call borrows ``frames``, ``out`` and ``offsets`` until the lane's work is done,
         as the reference's detector borrows its image for the call (src/fast_simd.rs:847):
-        each is recorded on the lane's stream (``Tensor.record_stream``), so torch's caching
-        allocator does not hand their memory to another tensor while the lane still reads or
-        writes it, even when the caller drops its last reference right after this call."""
+        the lane keeps a reference to each until its stream has passed the call, so torch's
+        caching allocator cannot hand their memory to another tensor while the lane still
+        reads or writes it, even when the caller drops its last reference right after this
+        call."""
         import torch
 
         lane = k % len(self.ctxs)
@@ -317,8 +336,7 @@ class Lanes:
             s.wait_stream(torch.cuda.current_stream(frames.device))
         detect_device(frames, config, out, offsets, stream=s, device=self.device,
                       ctx=self.ctxs[lane])
-        for t in (frames, out, offsets):
-            t.record_stream(s)
+        self._hold(lane, (frames, out, offsets))
         return lane
 
     def wait(self, lane=None):
@@ -330,9 +348,17 @@ class Lanes:
             cur.wait_stream(self.stream(i))
 
     def close(self):
+        """Wait for every lane, release the borrowed tensors, destroy the lanes' contexts
+        (lane 0 is the device's process-wide context and stays)."""
+        for i in range(len(self.ctxs)):
+            if self._held[i]:
+                self._held[i][-1][0].synchronize()
+                self._held[i].clear()
         for ctx in self.ctxs[1:]:
             ctx.close()
         self.ctxs = self.ctxs[:1]
+        self._ext = self._ext[:1]
+        self._held = self._held[:1]
 
 
 def detect_device_rgb(frames, config, out, offsets, stream=None, device=None):

@@ -3,16 +3,17 @@
 The reference's detector borrows its image for the length of a synchronous call
 (src/fast_simd.rs:847-859).  fast_hip.Lanes enqueues the call on a lane's own HIP stream and
 returns at once, so the borrow has to last until that stream is done: Lanes.detect_device
-records ``frames``, ``out`` and ``offsets`` on the lane's stream (Tensor.record_stream), and
-torch's caching allocator then keeps their memory out of reuse until the lane's work is done.
+keeps a reference to ``frames``, ``out`` and ``offsets`` until an event recorded after the call on
+the lane's stream has completed, so torch's caching allocator cannot reuse their memory
+before the lane's work is done.
 
 The test makes the hazard certain if the borrow is not honoured: every lane first waits behind
 a long spin kernel on a side stream, 30 calls are enqueued on freshly allocated batch tensors
 that are dropped right after the call, and between calls same-sized tensors are allocated and
 filled with 0xFF on torch's current stream (which is not blocked, so those fills run while the
 lanes still wait).  After lanes.wait() every result must equal the CPU oracle
-(oracle/fast_oracle.c, pinned to the reference's goldens).  The second test removes
-record_stream and shows that the same sequence then reads overwritten frames."""
+(oracle/fast_oracle.c, pinned to the reference's goldens).  The second test removes the
+borrow and shows that the same sequence then reads overwritten frames."""
 import numpy as np
 import pytest
 
@@ -54,7 +55,7 @@ def _run(torch, hosts, cfg, calls=30):
         outs, offs = [], []
         for k in range(calls):
             frames = torch.from_numpy(hosts[k % 3]).cuda()       # fresh, on the current stream
-            out = torch.full((NF * 60_000, 2), -1, dtype=torch.int32, device="cuda")
+            out = torch.full((NF * W * H // 2, 2), -1, dtype=torch.int32, device="cuda")
             off = torch.zeros(NF + 1, dtype=torch.int64, device="cuda")
             lanes.detect_device(k, frames, cfg, out, off)
             del frames                                             # the lane still needs it
@@ -85,15 +86,15 @@ def test_lanes_borrow_until_done(nms):
             assert np.array_equal(got, want[k % 3][f]), (k, f, len(got), len(want[k % 3][f]))
 
 
-def test_without_record_stream_the_hazard_is_real(monkeypatch):
-    """The same sequence with Tensor.record_stream made a no-op: the lanes read frames whose
-    memory the allocator has handed to the 0xFF fills (the test above would then fail).
-    Skipped, not failed, if this allocator happens not to reuse the blocks."""
+def test_without_the_borrow_the_hazard_is_real(monkeypatch):
+    """The same sequence with the lanes' borrow removed (Lanes._hold a no-op): the lanes read
+    frames whose memory the allocator has handed to the 0xFF fills (the test above would then
+    fail).  Skipped, not failed, if this allocator happens not to reuse the blocks."""
     import torch
 
     hosts = _hosts()
     want = [[oracle.detect(h[f], 16, 9, 1) for f in range(NF)] for h in hosts]
-    monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None)
+    monkeypatch.setattr(fast_hip.Lanes, "_hold", lambda self, lane, tensors: None)
     res = _run(torch, hosts, Config(16, 9, NonMaximalSuppression(1)))
     bad = sum(not np.array_equal(p[o[f]:o[f + 1]].astype(np.uint32), want[k % 3][f])
               for k, (o, p) in enumerate(res) for f in range(NF))
