@@ -11,7 +11,7 @@
 // and sweep them top to bottom:
 //   * lane l owns 16 columns (one 16-byte buffer load per row); lanes 0 and 63 are halo
 //     lanes that only feed their neighbours, so a strip covers 62 x 16 centres;
-//   * pixel rows stream through a register ring of kSweepRing slots: kSweepRing - 4 row loads
+//   * pixel rows stream through a register ring of kRing slots: kRing - 4 row loads
 //     are in flight, none is guarded by a branch and none is copied, so the compiler's vmcnt
 //     bookkeeping keeps them in flight;
 //   * every pairwise comparison is made once and used by both of its pixels: the vertical
@@ -50,6 +50,18 @@ namespace FDF_SWEEP_NS {
 
 // RGB8 input: 3 bytes per pixel, converted to luma as image 0.24.6 to_luma8 on load
 constexpr bool kRgb = FDF_SWEEP_RGB != 0;
+// The row ring and the occupancy target of this translation unit's kernels (kSweepRing /
+// kSweepWavesPerEU: 8 slots, 4 waves per SIMD, unless the unit overrides them).  A 16-slot
+// ring at 2 waves per SIMD for frames read in place over PCIe was measured slower (DESIGN.md
+// §7.5: PCIe read throughput, not latency, bounds that kernel).
+#ifndef FDF_SWEEP_TU_RING
+#define FDF_SWEEP_TU_RING kSweepRing
+#endif
+#ifndef FDF_SWEEP_TU_WAVES
+#define FDF_SWEEP_TU_WAVES kSweepWavesPerEU
+#endif
+constexpr int kRing = FDF_SWEEP_TU_RING;
+constexpr int kWavesEU = FDF_SWEEP_TU_WAVES;
 constexpr int kPx = kRgb ? 3 : 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -574,6 +586,24 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
     inflight[QL] = false;
 }
 
+// A/B variant (FDF_MAX_AGE > 0, off in the product): issue a partial
+// batch once the oldest queued candidate is FDF_MAX_AGE rows old, so its gathers read rows the
+// wave streamed recently enough to still be in L2.  `step` is the unit-relative row being
+// swept; the FIFO head entry's code holds its row (spread_code((row - ys) << 6 | lane)).
+#ifndef FDF_MAX_AGE
+#define FDF_MAX_AGE 0
+#endif
+__device__ __forceinline__ bool issue_aged(const SweepShared& sh, const UnitCtx& u, int step) {
+    if constexpr (FDF_MAX_AGE > 0) {
+        if (u.tail == u.head) return false;
+        const uint32_t e0 = __builtin_amdgcn_readfirstlane(sh.pq[u.head & (kSweepPixelQ - 1)]);
+        const int row = (int)(pack_nibbles(e0 & ~kFlagNibbles) >> 6);
+        return step - row >= FDF_MAX_AGE;
+    }
+    (void)sh; (void)u; (void)step;
+    return false;
+}
+
 template <int NMS, int N, bool EXACT>
 __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     constexpr int LC = kLaneCols;
@@ -609,12 +639,12 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
 #pragma unroll
     for (int q = 0; q < kSweepBatchSlots; ++q) inflight[q] = false;
 
-    // One kSweepRing-slot ring of pixel rows: row r in slot (r - ys) % kSweepRing.  At step J
-    // (row yv) it holds rows yv .. yv+K-2 (K = kSweepRing) with yv+4 .. yv+K-2 still loading,
+    // One kRing-slot ring of pixel rows: row r in slot (r - ys) % kRing.  At step J
+    // (row yv) it holds rows yv .. yv+K-2 (K = kRing) with yv+4 .. yv+K-2 still loading,
     // and row yv+K-1 is loaded into the slot of row yv-1, which is dead.  Nothing is copied,
     // so every slot keeps its registers across loop iterations and no wait is needed for a
     // register move.  The loop body is K steps, so unit sweeps are whole multiples of K.
-    constexpr int K = kSweepRing;
+    constexpr int K = kRing;
     RowV Rw[K];
     // The N flags of rows p0 .. p0+2 come from the vertical comparisons of rows p0-3 .. p0-1
     // with them, which the steps of those rows would have made: a prologue makes only those
@@ -710,7 +740,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 inflight[q] = false;                                                         \
             }                                                                                \
             if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                                  \
-            batch[q] = issue_batch<LC>(sh, u, false);                                        \
+            batch[q] = issue_batch<LC>(sh, u, issue_aged(sh, u, i0 + (J)));                  \
             inflight[q] = batch[q].n != 0;                                                   \
         }                                                                                    \
     }
@@ -1413,10 +1443,10 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     return total;
 }
 
-// Occupancy target: kSweepWavesPerEU waves per SIMD (4: 128 VGPRs each, 2: 256).
+// Occupancy target: kWavesEU waves per SIMD (4: 128 VGPRs each, 2: 256).
 template <int NMS, int N>
 __global__ __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(kSweepWavesPerEU, kSweepWavesPerEU)))
+__attribute__((amdgpu_waves_per_eu(kWavesEU, kWavesEU)))
 void fast_sweep_kernel(BandParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     uint64_t t0 = 0, r0 = 0;
@@ -1473,9 +1503,11 @@ typedef void (*SweepKernelFn)(BandParams);
 
 template <int NMS>
 static SweepKernelFn pick_sweep_n(uint32_t n) {
-#ifdef FDF_ISA_ONE_N   // ISA studies only (tools/isa_loops.py): one count per NMS mode, fast to compile
+#if defined(FDF_ISA_ONE_N)   // ISA studies only (tools/isa_loops.py): one count per NMS mode
     return n == FDF_ISA_ONE_N ? fast_sweep_kernel<NMS, FDF_ISA_ONE_N> : nullptr;
-#endif
+#elif defined(FDF_AB_COUNTS)   // A/B variant builds (tools/build_variant.sh): the bench's n = 9, 12
+    return n == 9 ? fast_sweep_kernel<NMS, 9> : (n == 12 ? fast_sweep_kernel<NMS, 12> : nullptr);
+#else
     switch (n) {
         case 9: return fast_sweep_kernel<NMS, 9>;
         case 10: return fast_sweep_kernel<NMS, 10>;
@@ -1487,6 +1519,7 @@ static SweepKernelFn pick_sweep_n(uint32_t n) {
         case 16: return fast_sweep_kernel<NMS, 16>;
         default: return nullptr;
     }
+#endif
 }
 
 static SweepKernelFn pick_sweep(uint32_t nms, uint32_t n) {
