@@ -62,6 +62,9 @@ def parse_args(argv=None):
     p.add_argument("--no-extras", action="store_true", help="skip the latency/leg extras")
     p.add_argument("--no-parity", action="store_true",
                    help="skip the whole-batch parity check of the headline (experiments only)")
+    p.add_argument("--copies", type=int, default=0,
+                   help="input copies of the shard (0 = one per lane and >= 512 MiB in all; "
+                        "1 = every lane reads the same copy, the rounds-1-4 protocol, for A/Bs)")
     p.add_argument("--lanes", type=int, default=3,
                    help="launch lanes: step k runs on lane k %% L, each lane a context with its "
                         "own HIP stream and no dependency between lanes (fast_hip.Lanes)")
@@ -502,11 +505,12 @@ def n_copies(batch_bytes, lanes, min_bytes):
     return -(-need // lanes) * lanes
 
 
-def make_batch(workloads, first, count, W, H, device, min_bytes=0, lanes=1):
-    """`count` S1 frames from global index `first` in n_copies(...) distinct copies: copy c
-    holds frames first + 211 c ... (each frame rolled differently from the same position in
-    every other copy).  Step k reads copy k % len(copies) on lane k % lanes."""
-    nc = n_copies(count * W * H, lanes, min_bytes)
+def make_batch(workloads, first, count, W, H, device, min_bytes=0, lanes=1, copies=0):
+    """`count` S1 frames from global index `first` in n_copies(...) distinct copies (or
+    `copies` when given): copy c holds frames first + 211 c ... (each frame rolled differently
+    from the same position in every other copy).  Step k reads copy k % len(copies) on lane
+    k % lanes."""
+    nc = copies if copies > 0 else n_copies(count * W * H, lanes, min_bytes)
     return [workloads.s1_frames_torch(first + COPY_ROLL * c, count, W, H, device=device)
             for c in range(nc)]
 
@@ -740,7 +744,7 @@ def main(argv=None):
     # same bytes), and >= 512 MiB in all, so that its frames come from HBM, not the 256 MiB
     # Infinity Cache
     copies = make_batch(workloads, first, count, W, H, device, min_bytes=1 << 29,
-                        lanes=args.lanes)
+                        lanes=args.lanes, copies=args.copies)
     frames = copies[0]
     cap = max(count, 1) * 200_000
     stream = torch.cuda.current_stream(device)

@@ -248,7 +248,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     // LDS per workgroup sets the workgroups per CU: <= 40 KB keeps 4.
     // Without NMS a 35 KB budget (bands of ~122 rows at 1080p) measured faster than the
     // tallest band that fits (more, shorter workgroups: a shorter grid tail).
-    uint32_t budget = nms ? 40000u : 35000u;
+    uint32_t budget = (nms ? 40000u : 35000u) + 4 * fdfk::kWinBytes;
 #ifdef FDF_DEBUG_BUILD
     if (const char* b = std::getenv("FDF_LDS_BUDGET"))
         budget = std::min<uint32_t>(fdfk::kSweepMaxLds, (uint32_t)std::strtoul(b, nullptr, 0));
@@ -400,8 +400,9 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     }
     // workgroup slots of the device: 4 per CU (4 waves per SIMD); fdf_ctx_set_geometry's
     // min_tasks replaces it (1: the tall bands of a large batch for any job)
+    const uint64_t per_cu = fdfk::kWinBytes ? 2ull : 4ull;    // FDF_LDS_WINDOW: 2 per CU
     const uint64_t slots = ctx->min_tasks ? ctx->min_tasks
-                                          : (ctx->cus ? 4ull * ctx->cus : kDefaultMinTasks);
+                                          : (ctx->cus ? per_cu * ctx->cus : kDefaultMinTasks);
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows);
     const uint32_t R = geo.R;
     const uint32_t nw = fdfk::bitmap_words_per_row(w);

@@ -199,6 +199,7 @@ struct SweepShared {
     uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
     const uint32_t* seltab;  // select_bit's table (SweepLayout::seltab)
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
+    uint8_t* win;          // FDF_LDS_WINDOW: this wave's ring of kWinRows pixel rows
 };
 
 struct UnitCtx {
@@ -325,6 +326,30 @@ __device__ __forceinline__ FifoPeek fifo_peek(const SweepShared& sh, const UnitC
     return f;
 }
 
+#ifdef FDF_LDS_WINDOW
+// The 7 row windows of centre (strip column cl, unit row rr + 3) from the wave's LDS ring: ring
+// row (rel % kWinRows) holds unit-relative row rel = row - (ys - 3), 64 lanes x 16 bytes, byte
+// cl = strip column cl.  Rows rr .. rr + 6 wrap at most once.  Unaligned 32-bit LDS reads.
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t* p) {
+    return *reinterpret_cast<const uint32_t*>(p);
+}
+__device__ __forceinline__ void load_ring_windows_lds(Batch& b, const uint8_t* win, uint32_t rr,
+                                                      uint32_t cl) {
+    const uint32_t s0 = rr - kWinRows * ((rr * 6554u) >> 16);   // rr % 10 for rr < 2^14
+    const uint8_t* base = win + s0 * 1024u + cl;
+    const uint8_t* wrap = base - kWinRows * 1024u;
+    const uint32_t k = kWinRows - s0;                            // first row that wraps
+    auto row = [&](uint32_t d) { return (d < k ? base : wrap) + d * 1024u; };
+    b.a0 = lds_u32(row(0) - 1);
+    b.a1 = u32x2{lds_u32(row(1) - 2), lds_u32(row(1) + 2)};
+    b.a2 = u32x2{lds_u32(row(2) - 3), lds_u32(row(2) + 1)};
+    b.a3 = u32x2{lds_u32(row(3) - 3), lds_u32(row(3) + 1)};
+    b.a4 = u32x2{lds_u32(row(4) - 3), lds_u32(row(4) + 1)};
+    b.a5 = u32x2{lds_u32(row(5) - 2), lds_u32(row(5) + 2)};
+    b.a6 = lds_u32(row(6) - 1);
+}
+#endif
+
 template <int LC>
 __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, bool force,
                                              const FifoPeek& pk) {
@@ -335,6 +360,7 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
     b.code = 0;
     const int W = (int)u.src.W;
     int o = 3;                                        // pixel (x, y - 3) of centre (3, 3)
+    uint32_t wrr = 0, wcl = 16;                       // FDF_LDS_WINDOW: ring row, strip column
     const uint32_t nent = pk.nent;
     if (nent != 0) {
         const uint32_t lane = u.lane;
@@ -385,10 +411,20 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
                 b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
                 // rows relative to the unit (< 2^10) times W (< 2^16): a 24-bit multiply
                 o = u.rowbase + (int)__umul24(sc >> 10, (uint32_t)W) + u.S - LC + (int)(sc & 1023u);
+                wrr = sc >> 10;
+                wcl = sc & 1023u;
             }
         }
     }
+#ifdef FDF_LDS_WINDOW
+    (void)o;
+    // the ring rows other lanes wrote this step (see the staging fence above)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    load_ring_windows_lds(b, sh.win, wrr, wcl);
+#else
+    (void)wrr; (void)wcl;
     load_ring_windows(b, u.src.rs, o, W);
+#endif
     return b;
 }
 
@@ -655,6 +691,18 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     for (int k = 0; k < 3; ++k) up[k] = load_row<LC, EXACT>(u.src, ys - 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
+#ifdef FDF_LDS_WINDOW
+    // the ring of the last kWinRows rows: unit row rel = row - (ys - 3) in ring row rel % 10;
+    // the prologue's rows ys - 3 .. ys + 2 first, then each step writes its row yv + 3
+    const uint32_t lane16 = lane * 16u;
+    auto win_put = [&](uint32_t rel, const RowV& v) {
+        *reinterpret_cast<RowV*>(sh.win + (rel % kWinRows) * 1024u + lane16) = v;
+    };
+#pragma unroll
+    for (int k = 0; k < 3; ++k) win_put((uint32_t)k, up[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) win_put((uint32_t)(k + 3), Rw[k]);
+#endif
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 #pragma unroll
     for (int k = 0; k < 3; ++k) V[k + 1] = compare_rows<LC>(Rw[k], ~up[k], lk);
@@ -670,6 +718,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
+        FDF_WIN_PUT(i0 + (J) + 6, s);                                                        \
         const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
         {                                                                                    \
             RowV e;                                                                          \
@@ -732,7 +781,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, true));    \
             }                                                                                \
         }                                                                                    \
-        if (((J) % kIssue) == kIssue - 1) {                                                  \
+        if (((J) % kIssue) == kIssue - 1 || (kWindowed && (J) == K - 1)) {                   \
             /* the batch of this slot is due; issue the next full one into it */             \
             constexpr int q = ((J) / kIssue) % kSweepBatchSlots;                             \
             if (inflight[q]) {                                                               \
@@ -740,12 +789,30 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 inflight[q] = false;                                                         \
             }                                                                                \
             if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                                  \
-            batch[q] = issue_batch<LC>(sh, u, issue_aged(sh, u, i0 + (J)));                  \
+            if constexpr (kWindowed) {                                                       \
+                /* LDS window: every queued candidate goes now (its rows leave the ring */   \
+                /* soon); all but the last batch are tested at once */                       \
+                Batch nb = issue_batch<LC>(sh, u, true);                                     \
+                while (u.tail != u.head) {                                                   \
+                    evaluate_batch<NMS, N, LC>(sh, u, lk, nb);                               \
+                    nb = issue_batch<LC>(sh, u, true);                                       \
+                }                                                                            \
+                batch[q] = nb;                                                               \
+            } else {                                                                         \
+                batch[q] = issue_batch<LC>(sh, u, issue_aged(sh, u, i0 + (J)));              \
+            }                                                                                \
             inflight[q] = batch[q].n != 0;                                                   \
         }                                                                                    \
     }
 
     static_assert(K == 8 || K == 16, "ring of 8 or 16 rows (a power of two: row codes OR together)");
+#ifdef FDF_LDS_WINDOW
+    constexpr bool kWindowed = true;
+#define FDF_WIN_PUT(rel, v) win_put((uint32_t)(rel), v)
+#else
+    constexpr bool kWindowed = false;
+#define FDF_WIN_PUT(rel, v)
+#endif
     static_assert((K / kIssue) % kSweepBatchSlots == 0 || kSweepBatchSlots == 1,
                   "issue points per loop body must cycle through the batch slots");
     for (int i0 = 0; i0 < T; i0 += K) {
@@ -773,6 +840,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         }
     }
 #undef FDF_SWEEP_STEP
+#undef FDF_WIN_PUT
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
@@ -1271,6 +1339,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
     sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
     sh.seltab = reinterpret_cast<const uint32_t*>(smem_raw + L.seltab);
+    sh.win = smem_raw + L.win + wave * kWinBytes;
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;

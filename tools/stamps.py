@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--nms", default="maxt")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--raw", default="", help="write the raw stamps of each batch size here (.npz)")
+    ap.add_argument("--host", default="", choices=["", "pinned", "copy"],
+                    help="one frame through fdf_detect instead: 'pinned' = read in place from "
+                         "pinned host memory, 'copy' = the same buffer copied to the device first")
     args = ap.parse_args()
     import torch
 
@@ -120,6 +123,33 @@ def main():
     ctx = fast_hip.context(0)
     res = {}
     raw = {}
+    if args.host:
+        frame = workloads.s1_frame(0, args.width, args.height)
+        pin = torch.from_numpy(frame).pin_memory()
+        cap = args.width * args.height // 8
+        pout = torch.empty((cap, 2), dtype=torch.int32).pin_memory()
+        c = _native.FdfConfig(args.threshold, args.count, nms)
+        ctx.set_upload_chunks(1 if args.host == "copy" else 0)
+        per = []
+        for k in range(5 + args.iters):
+            n = ctypes.c_size_t(0)
+            _native.check(lib.fdf_detect(ctx.handle, pin.data_ptr(), args.width, args.height,
+                                         args.width, ctypes.byref(c), pout.data_ptr(), cap,
+                                         ctypes.byref(n)), "fdf_detect")
+            if k < 5:
+                continue
+            m = ctypes.c_uint64(0)
+            _native.check(lib.fdf_debug_stamps(ctx.handle, None, 0, ctypes.byref(m)), "stamps")
+            buf = np.zeros(m.value, dtype=np.uint64)
+            _native.check(lib.fdf_debug_stamps(ctx.handle, buf.ctypes.data, m.value,
+                                               ctypes.byref(m)), "stamps")
+            st = buf.reshape(-1, WORDS).astype(np.int64)
+            per.append(summarize(st, st.shape[0]))
+        ctx.set_upload_chunks(0)
+        med = sorted(per, key=lambda d: d["span_us"])[len(per) // 2]
+        med["span_us_all"] = [p["span_us"] for p in per]
+        print(json.dumps({"config": vars(args), "host_frame": med}, indent=1))
+        return
     for F in args.frames:
         frames = workloads.s1_frames_torch(0, F, args.width, args.height)
         # copies so that the batch comes from HBM, not the Infinity Cache (as bench.py)
