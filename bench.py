@@ -176,23 +176,26 @@ def barrier(world):
         dist.barrier()
 
 
-def load_traffic(cfg_key):
+def load_traffic(cfg_key, lanes=1):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/
-    pmc_traffic.json), and the entry's stamp: (bytes, {"src_sha16", "rev", "stale"}).  An
-    entry profiled from other kernel sources than the ones in this tree is stale: its bytes
-    are not reported (None) and the stamp says so."""
+    pmc_traffic.json), and the entry's stamp: (bytes, {"src_sha16", "rev", "stale", "key"}).
+    With lanes > 1 the entry profiled under that many lanes (each reading its own input copy,
+    tools/profile_round.sh) is preferred.  An entry profiled from other kernel sources than
+    the ones in this tree is stale: its bytes are not reported (None) and the stamp says so."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            entry = json.load(f).get(cfg_key, {})
+            data = json.load(f)
     except (OSError, ValueError):
-        entry = {}
+        data = {}
+    key = f"{cfg_key}_lanes{lanes}" if lanes > 1 and f"{cfg_key}_lanes{lanes}" in data else cfg_key
+    entry = data.get(key, {})
     if not entry:
         return None, None
     import workloads
     now = workloads.kernel_source_sha16()
     stamp = {"src_sha16": entry.get("src_sha16"), "rev": entry.get("rev"),
-             "stale": entry.get("src_sha16") != now}
+             "stale": entry.get("src_sha16") != now, "key": key}
     return (None if stamp["stale"] else entry.get("hbm_bytes_per_launch")), stamp
 
 def gpu_clocks(device_index):
@@ -785,7 +788,7 @@ def main(argv=None):
     in_bytes = count * W * H
     alg_bytes = in_bytes + 8 * total_kp + 4 * count
     cfg_key = f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{args.nms}"
-    roofline = roofline_of(tm, alg_bytes, in_bytes, load_traffic(cfg_key))
+    roofline = roofline_of(tm, alg_bytes, in_bytes, load_traffic(cfg_key, len(lanes)))
 
     extras = {}
     cpu = None
@@ -808,7 +811,8 @@ def main(argv=None):
                    "ms_per_step": round(e2 * 1e3 / args.steps, 4),
                    "keypoints_per_step": int(reduce_sum(float(kp2), world, device)),
                    "roofline": roofline_of(t2, in_bytes + 8 * kp2 + 4 * count, in_bytes,
-                                           load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}")),
+                                           load_traffic(f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{other}",
+                                                        len(lanes))),
                    "parity": par2}
             extras[f"nms_{other}"] = leg
         # the same batch on one lane (one stream: every launch waits for the previous call's
