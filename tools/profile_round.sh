@@ -29,4 +29,6 @@ KEY=$(python3 -c "import json,sys; c=json.load(open('$O/fetch_l1.json'))['config
 python3 tools/traffic_json.py "$O/fetch_l1" "$O/write_l1" "$KEY" "$O/pmc_traffic.json"
 python3 tools/traffic_json.py "$O/fetch_l3" "$O/write_l3" "${KEY}_lanes3" "$O/pmc_traffic.json"
 find "$O/stats" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
+# the raw traces and counter rows stay on the box (gpurun copies back <= 64 MiB)
+rm -rf "$O/stats" "$O"/fetch_l? "$O"/write_l? "$O/tcc_l3"
 echo "profile done: $O"
