@@ -380,6 +380,7 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
     # algorithmic bytes as the headline's: W*H + 8K + 4 per frame
     alg = in_bytes + 8 * kp_step + 4 * frames
     per_launch = t.span_ms / steps
+    tbytes, tstamp = load_traffic(f"{W}x{H}_b{frames}_t8_n12_sad", len(lanes))
     det1 = float(np.mean(t1.det)) if len(t1.det) else None
     res = {"workload": f"batch of {frames} {W}x{H} S1 frames, t=8 n=12 nms=sad, "
                        f"{len(copies)} distinct copies (one per lane)",
@@ -392,6 +393,8 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
            "alg_bytes_per_launch": int(round(alg)),
            "roofline_frac": round(alg / (per_launch * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "roofline_frac_input_bytes_only": round(in_bytes / (per_launch * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "traffic": tbytes, "traffic_stamp": tstamp,
+           "traffic_over_alg": round(tbytes / alg, 3) if tbytes else None,
            "single_lane": {"ms_per_step": round(t1.elapsed * 1e3 / steps, 4),
                            "kernel_ms_avg": round(det1, 4) if det1 else None,
                            "kernel_ms": percentiles(t1.det) if len(t1.det) >= MIN_TIMED else None,
@@ -631,6 +634,7 @@ def roofline_of(t, alg_bytes, in_bytes, traffic):
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tbytes,
             "traffic_stamp": tstamp,
+            "traffic_over_alg": round(tbytes / alg_bytes, 3) if tbytes else None,
             "kernel": "fast_sweep_kernel", "kernel_ms_avg": round(per_launch, 4),
             "kernel_ms_basis": f"HIP-event span of {t.steps} launches on {t.lanes} lane stream(s) / launches",
             "lanes": t.lanes,
