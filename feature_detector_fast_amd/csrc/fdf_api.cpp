@@ -231,7 +231,8 @@ struct Geometry {
 
 
 Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
-                       uint64_t slots, double density, uint32_t forced_rows) {
+                       uint64_t slots, double density, uint32_t forced_rows,
+                       bool host_src = false) {
     Geometry g;
     const uint32_t sc = (uint32_t)fdfk::strip_cols(fdfk::kLaneCols);
     g.nstrips = (w - 3 + sc - 1) / sc;
@@ -285,22 +286,49 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     constexpr double kUnitCost = 3.0;
     const double band_cost = nms ? 4.0 : 2.0;
     const uint32_t units_per_wave = (g.nstrips * g.nsub + fdfk::kWaves - 1) / fdfk::kWaves;
-    auto wg_cost = [&](uint32_t rows) {
+    // A grid that fits one round of the chip (a single frame) is latency-bound, one wave per
+    // SIMD: a unit's padding steps past its last row (the sweep runs whole 8-step blocks) load
+    // nothing and cost a quarter of a real step, and every band's look-back polls the
+    // descriptors of the bands before it, one round per 64.  Measured on one device-resident
+    // 1080p frame (profiles/r05/e7_single_frame_rows/, sweep us at 4 / 6 / 8 / 10 / 14 / 20 rows):
+    // max-t 19.0 / 17.2 / 17.8 / 18.1 / 19.4 / 22.6, NMS off 15.0 / 13.3 / 13.4 / 13.5 / 13.9 /
+    // 17.1 -- this model picks 6 rows for both (14 and 16 before).  A frame read in place over
+    // PCIe keeps the full-step model: its halo rows cost PCIe bytes, and 6-10 rows measured
+    // within noise of 14 there (r5_e8_host_rows_*.json).
+    auto wg_cost = [&](uint32_t rows, bool latency) {
         const uint32_t unit_rows = (rows + g.nsub - 1) / g.nsub;
-        return units_per_wave * ((double)fdfk::sweep_steps(unit_rows, halo) + kUnitCost) + band_cost;
+        const double steps = (double)fdfk::sweep_steps(unit_rows, halo);
+        const double real = std::min(steps, (double)(unit_rows + halo));
+        return units_per_wave * ((latency ? real + 0.25 * (steps - real) : steps) + kUnitCost) +
+               band_cost;
     };
-    double best = 0.0;
-    g.R = 0;
-    for (uint32_t R = g.nsub; R <= max_rows && R < centre_rows + g.nsub; R += g.nsub) {
-        if (fdfk::make_sweep_layout(R, nw, nms).total > budget) break;
-        const uint32_t bands = (centre_rows + R - 1) / R;
-        const double full = wg_cost(R), last = wg_cost(centre_rows - (bands - 1) * R);
-        const double total = (double)n_frames * ((bands - 1) * full + last);
-        const double t = std::max(total / (double)slots, full) + 0.5 * full;
-        if (g.R == 0 || t <= best * 1.001) {  // ties: the taller band (fewer workgroups)
-            best = t;
-            g.R = R;
+    const uint64_t one_round = std::min<uint64_t>(slots, fdfk::kDirectMaxTasks);
+    auto pick = [&](bool latency) {
+        double best = 0.0;
+        uint32_t best_R = 0;
+        for (uint32_t R = g.nsub; R <= max_rows && R < centre_rows + g.nsub; R += g.nsub) {
+            if (fdfk::make_sweep_layout(R, nw, nms).total > budget) break;
+            const uint32_t bands = (centre_rows + R - 1) / R;
+            const uint64_t ntasks = (uint64_t)n_frames * bands;
+            if (latency && ntasks > one_round) continue;   // stays one round of the chip
+            const double lookback = latency ? (double)((ntasks + 63) / 64) : 0.0;
+            const double full = wg_cost(R, latency) + lookback;
+            const double last = wg_cost(centre_rows - (bands - 1) * R, latency) + lookback;
+            const double total = (double)n_frames * ((bands - 1) * full + last);
+            const double t = std::max(total / (double)slots, full) + 0.5 * full;
+            if (best_R == 0 || t <= best * 1.001) {  // ties: the taller band (fewer workgroups)
+                best = t;
+                best_R = R;
+            }
         }
+        return best_R;
+    };
+    g.R = pick(false);
+    // the grid of that height fits one round of the chip: the latency model picks among the
+    // heights that keep it so
+    if (!host_src && g.R && (uint64_t)n_frames * ((centre_rows + g.R - 1) / g.R) <= one_round) {
+        const uint32_t r = pick(true);
+        if (r) g.R = r;
     }
     if (g.R == 0) g.R = g.nsub;
     return g;
@@ -369,7 +397,7 @@ struct ChunkedUpload {
 int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w, uint32_t h,
             uint64_t frame_stride, const fdf_config* cfg, uint2* d_out, uint64_t cap,
             uint64_t* d_offsets, hipStream_t stream, bool rgb = false,
-            const ChunkedUpload& up = ChunkedUpload{}) {
+            const ChunkedUpload& up = ChunkedUpload{}, bool host_src = false) {
     double density = 0.0;
     if (!ctx->h_stats) {
         void* hp = nullptr;
@@ -403,7 +431,8 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     const uint64_t per_cu = fdfk::kWinBytes ? 2ull : 4ull;    // FDF_LDS_WINDOW: 2 per CU
     const uint64_t slots = ctx->min_tasks ? ctx->min_tasks
                                           : (ctx->cus ? per_cu * ctx->cus : kDefaultMinTasks);
-    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows);
+    const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows,
+                                       host_src);
     const uint32_t R = geo.R;
     const uint32_t nw = fdfk::bitmap_words_per_row(w);
 #ifdef FDF_DEBUG_BUILD
@@ -797,7 +826,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
     rc = enqueue(ctx, in_place ? in_place : ctx->d_in, n_frames, w, h, frame_bytes, cfg,
-                 out_dev, *out_cap, offs_dev, ctx->stream, false, up);
+                 out_dev, *out_cap, offs_dev, ctx->stream, false, up, in_place != nullptr);
     if (chunked) {
         // the copies end before the detector does (it waits for the last one), but a failed
         // launch or a timed-out wait would leave them running: drain them before any return

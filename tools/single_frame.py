@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nms", default="maxt")
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--rows", type=int, default=0, help="fdf_ctx_set_band_rows (0 = automatic)")
     args = ap.parse_args()
     import torch
 
@@ -26,6 +27,7 @@ def main():
     offs = torch.zeros(2, dtype=torch.int64, device="cuda")
     cfg = Config(16, 9, NonMaximalSuppression(nms))
     stream = torch.cuda.current_stream()
+    fast_hip.context(0).set_band_rows(args.rows)
     for _ in range(20):
         fast_hip.detect_device(one, cfg, out, offs, stream=stream)
     torch.cuda.synchronize()
@@ -44,7 +46,7 @@ def main():
     ctx.set_timing(False)
     # back-to-back calls: the stream never idles, so the event span / calls is the throughput
     # latency; each call alone is bounded below by its two kernels
-    print(json.dumps({"nms": args.nms, "calls": args.iters,
+    print(json.dumps({"nms": args.nms, "calls": args.iters, "rows": args.rows,
                       "event_ms_per_call": round(s.elapsed_time(e) / args.iters, 4),
                       "host_wall_ms_per_call": round(wall, 4),
                       "sweep_ms_p50": round(float(sorted(det)[len(det) // 2]), 4),
