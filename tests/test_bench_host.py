@@ -82,3 +82,44 @@ def test_roofline_from_timed_region():
     few = bench.Timed(0.001, 1.0, [0.4] * 4, [0.01] * 4, 0, 4, 1)
     r4 = bench.roofline_of(few, alg, in_bytes, (None, None))
     assert r4["launch_ms"] is None and r4["compaction_kernel_ms"] is None    # mean only
+
+
+def test_batch_parity_checks_every_frame():
+    """bench.batch_parity on CPU tensors: each lane's last result equal to
+    the checker on every frame passes; one moved point in any frame of any lane fails, and so
+    do wrong offsets."""
+    import numpy as np
+    import torch
+
+    import workloads
+    from oracle import oracle
+
+    W, H, F = 160, 90, 5
+    copies = [torch.from_numpy(np.stack([workloads.s1_frame(i + 211 * c, W, H) for i in range(F)]))
+              for c in range(2)]
+    ref = [oracle.avx2_detect_batch(c, 16, 9, 1) for c in copies]
+
+    class Bufs:
+        pass
+
+    def bufs_from(refs):
+        b = Bufs()
+        b.out = [torch.from_numpy(np.concatenate([p.astype(np.int32), np.zeros((7, 2), np.int32)]))
+                 for p, _ in refs]
+        b.offs = [torch.from_numpy(o.astype(np.int64)) for _, o in refs]
+        return b
+
+    tm = bench.Timed(0.01, 1.0, [], [], 1, 4, 2, lane_copy={0: 0, 1: 1}, copy_steps={0: 2, 1: 2})
+    rec, kp = bench.batch_parity(oracle, copies, bufs_from(ref), tm, 16, 9, 1, W)
+    assert rec["bit_exact"] and rec["oracle_frames"] == "all" and rec["raster_order"]
+    assert kp == (ref[0][1][-1] + ref[1][1][-1]) / 2
+    assert [c["copy"] for c in rec["lanes_compared"]] == [0, 1]
+    # a point moved in the last frame of lane 1
+    bad = bufs_from(ref)
+    n = int(ref[1][1][-1])
+    bad.out[1][n - 1, 0] += 1
+    assert not bench.batch_parity(oracle, copies, bad, tm, 16, 9, 1, W)[0]["bit_exact"]
+    # offsets shifted between two frames of lane 0 (same points, wrong frame split)
+    bad = bufs_from(ref)
+    bad.offs[0][2] += 1
+    assert not bench.batch_parity(oracle, copies, bad, tm, 16, 9, 1, W)[0]["bit_exact"]
