@@ -890,6 +890,17 @@ def main(argv=None):
             extras[f"single_frame_{name}_ms_p50"] = round(lat[len(lat) // 2], 4)
             extras[f"single_frame_{name}_Mpix_s"] = round(ow * oh / (lat[len(lat) // 2] * 1e-3) / 1e6, 1)
             extras[f"single_frame_{name}_kp"] = int(offs[1].item())
+            # the detector's own duration per call (dispatch-timestamped events, no packets
+            # between the kernels): the events above also hold each call's dispatch gap
+            sf_ctx = fast_hip.context(device.index or 0)
+            sf_ctx.set_timing(True)
+            for _ in range(50):
+                fast_hip.detect_device(one, c1, out, offs, stream=stream)
+            torch.cuda.synchronize()
+            det, _ = sf_ctx.timing_samples()
+            sf_ctx.set_timing(False)
+            if len(det):
+                extras[f"single_frame_{name}_kernel_ms_p50"] = round(float(np.median(det)), 4)
         host = one[0].cpu().numpy()
         extras["host_fdf_detect_ms"] = host_latency(
             fast_hip, _native, host,
