@@ -1324,6 +1324,8 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
             __builtin_amdgcn_s_sleep(2);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // the invalidate completes asynchronously: the barrier below waits for it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if constexpr (kDebugBuild) ph[0] = __builtin_amdgcn_s_memtime();   // setup done

@@ -67,6 +67,7 @@ def main():
         res[key] = {"p5": q(0.05), "p50": q(0.5), "p95": q(0.95), "keypoints": n.value}
     ctx.set_band_rows(0)
     ctx.set_upload_chunks(0)
+    res["recoveries"] = list(ctx.recoveries())    # (upload fallbacks, look-back recoveries)
     print(json.dumps(res))
 
 
