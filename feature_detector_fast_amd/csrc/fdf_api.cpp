@@ -602,18 +602,10 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         }
         ev = &ctx->ev[4 * ctx->timed];
     }
-    // a small grid whose units are shorter than one 8-step block (a single frame's latency
-    // bands) runs the instances that leave the block at the unit's last row
-    // (fdf_sweep_latency.hip; 1080p NMS off 13.5 -> 12.5 us, max-t 17.3 -> 17.0 us per frame).
-    // Long units keep whole blocks: the exit tests cost the batch loop more than the padding
-    // steps they save (512 x 1080p NMS off, 61-row units: +0.6 %, profiles/r05/e16_*)
-    const uint32_t unit_steps = (R + geo.nsub - 1) / geo.nsub +
-                                fdfk::band_halo(cfg->nms) * (geo.nsub == 1 ? 2u : 1u);
-    const bool exit_in_block = !rgb && direct && unit_steps < fdfk::kSweepRing;
-    auto launch = rgb ? fdfk::launch_sweep_rgb
-                      : (exit_in_block ? fdfk::launch_sweep_latency : fdfk::launch_sweep);
-    if (launch(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr) !=
-        hipSuccess) {
+    if ((rgb ? fdfk::launch_sweep_rgb(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr,
+                                      ev ? ev[1] : nullptr)
+             : fdfk::launch_sweep(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr,
+                                  ev ? ev[1] : nullptr)) != hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }

@@ -245,10 +245,6 @@ hipError_t launch_compact(const CompactParams& c, hipStream_t stream, hipEvent_t
                           hipEvent_t stop = nullptr);
 hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
                         hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
-// The same detector whose units leave their last 8-step block at their last row
-// (fdf_sweep_latency.hip): for grids of short units (a single frame's latency bands)
-hipError_t launch_sweep_latency(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
-                                hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // Workgroups of the detector instance (nms, n; grey or RGB) one CU holds at once with
 // `lds_bytes` of dynamic LDS (the runtime's occupancy calculator: registers, LDS, waves).
 hipError_t sweep_occupancy(uint32_t nms, uint32_t n, uint32_t lds_bytes, bool rgb, int* wg_per_cu);

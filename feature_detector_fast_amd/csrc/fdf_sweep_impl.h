@@ -1,9 +1,7 @@
 // fdf_sweep_impl.h -- column-sweep FAST-9..16 kernel for MI355X (gfx950), the production path.
-// Included by fdf_sweep.hip (grey frames: FDF_SWEEP_RGB 0, namespace fdfk::grey),
-// fdf_sweep_latency.hip (grey frames, units leave their last 8-step block early: namespace
-// fdfk::grey_lat) and fdf_sweep_rgb.hip (RGB8 frames converted to luma in the row and window
-// loads: FDF_SWEEP_RGB 1, namespace fdfk::rgb); each translation unit instantiates its 24
-// kernels.
+// Included by fdf_sweep.hip (grey frames: FDF_SWEEP_RGB 0, namespace fdfk::grey) and
+// fdf_sweep_rgb.hip (RGB8 frames converted to luma in the row and window loads:
+// FDF_SWEEP_RGB 1, namespace fdfk::rgb); each translation unit instantiates its 24 kernels.
 //
 // Replaces detect<NONMAX>() (iwanders/feature_detector_fast src/fast_simd.rs:301-620) with
 // determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
@@ -64,14 +62,6 @@ constexpr bool kRgb = FDF_SWEEP_RGB != 0;
 #endif
 constexpr int kRing = FDF_SWEEP_TU_RING;
 constexpr int kWavesEU = FDF_SWEEP_TU_WAVES;
-// Units that end inside an 8-step block leave it at their last row (FDF_SWEEP_TU_EXIT, the
-// latency instances of fdf_sweep_latency.hip: a single frame's 3-row units skip 4 padding
-// steps).  The exit tests perturb the long-unit loop's code (512 x 1080p max-t +0.5..+2 %,
-// DESIGN.md §7.6), so the throughput instances keep whole blocks.
-#ifndef FDF_SWEEP_TU_EXIT
-#define FDF_SWEEP_TU_EXIT 0
-#endif
-constexpr bool kExitInBlock = FDF_SWEEP_TU_EXIT != 0;
 constexpr int kPx = kRgb ? 3 : 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -828,31 +818,26 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     for (int i0 = 0; i0 < T; i0 += K) {
         // FIFO code of row ys + i0 + J: i0 is a multiple of K, so its spread ORs with J's
         const uint32_t lane_row_code = lane_code | spread_code((uint32_t)i0 << 6);
-        // (latency instances: leave the block after the unit's last row, wave-uniform)
-#define FDF_STEP_EXIT(J) if constexpr (kExitInBlock) { if (i0 + (J) + 1 >= T) break; }
-        FDF_SWEEP_STEP(0) FDF_STEP_EXIT(0)
-        FDF_SWEEP_STEP(1) FDF_STEP_EXIT(1)
-        FDF_SWEEP_STEP(2) FDF_STEP_EXIT(2)
-        FDF_SWEEP_STEP(3) FDF_STEP_EXIT(3)
-        FDF_SWEEP_STEP(4) FDF_STEP_EXIT(4)
-        FDF_SWEEP_STEP(5) FDF_STEP_EXIT(5)
-        FDF_SWEEP_STEP(6) FDF_STEP_EXIT(6)
+        FDF_SWEEP_STEP(0)
+        FDF_SWEEP_STEP(1)
+        FDF_SWEEP_STEP(2)
+        FDF_SWEEP_STEP(3)
+        FDF_SWEEP_STEP(4)
+        FDF_SWEEP_STEP(5)
+        FDF_SWEEP_STEP(6)
         FDF_SWEEP_STEP(7)
         if constexpr (K >= 12) {
-            FDF_STEP_EXIT(7)
-            FDF_SWEEP_STEP(8) FDF_STEP_EXIT(8)
-            FDF_SWEEP_STEP(9) FDF_STEP_EXIT(9)
-            FDF_SWEEP_STEP(10) FDF_STEP_EXIT(10)
+            FDF_SWEEP_STEP(8)
+            FDF_SWEEP_STEP(9)
+            FDF_SWEEP_STEP(10)
             FDF_SWEEP_STEP(11)
         }
         if constexpr (K >= 16) {
-            FDF_STEP_EXIT(11)
-            FDF_SWEEP_STEP(12) FDF_STEP_EXIT(12)
-            FDF_SWEEP_STEP(13) FDF_STEP_EXIT(13)
-            FDF_SWEEP_STEP(14) FDF_STEP_EXIT(14)
+            FDF_SWEEP_STEP(12)
+            FDF_SWEEP_STEP(13)
+            FDF_SWEEP_STEP(14)
             FDF_SWEEP_STEP(15)
         }
-#undef FDF_STEP_EXIT
     }
 #undef FDF_SWEEP_STEP
 #undef FDF_WIN_PUT
