@@ -32,8 +32,6 @@ struct LastResult {
     bool rgb = false;              // frames in d_rgb (RGB8); scores need their luma in d_in
     bool in_place = false;         // the frame was read in place from pinned host memory: not
                                    // in d_in, so the result has no scores (fdf_fetch_last)
-    bool in_user = false;          // the points went straight into the caller's pinned buffer
-                                   // (not h_out: fdf_fetch_last compacts them again)
     // fdf_detect_batch_multi: the call's generation (0: not a multi-context result) and this
     // context's shard of it, checked by fdf_fetch_last_multi
     uint64_t multi_gen = 0;
@@ -663,7 +661,7 @@ int check_host_args(const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t
 // with image 0.24.6's to_luma8 before detection (src/main.rs:58).
 int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
              size_t row_stride, size_t frame_stride, const fdf_config* cfg, bool rgb,
-             uint64_t* offs, bool host_out, uint2* user_out = nullptr, size_t user_cap = 0) {
+             uint64_t* offs, bool host_out) {
     ctx->last = LastResult{};          // invalid, and not a shard of a multi-context call
     const size_t frame_bytes = (size_t)w * h;
     const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
@@ -683,10 +681,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         out_dev = ctx->hd_out;
         offs_dev = ctx->hd_offs;
         out_cap = &ctx->h_out_points;
-        if (user_out) {                // the caller's pinned buffer, written by the kernels
-            out_dev = user_out;
-            out_cap = &user_cap;
-        }
     } else {
         if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, guess, ctx->stream))) return rc;
         if ((rc = ensure(ctx, &ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, ctx->stream)))
@@ -887,7 +881,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (size_t)total, ctx->stream))) return rc;
             c.out = ctx->d_out;
         }
-        c.cap = host_out ? ctx->h_out_points : ctx->out_points;
+        c.cap = *out_cap;
         c.kp_stats = nullptr;           // already reported (and reset) by the first compaction
         if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
             hipEventRecord(ctx->done, ctx->stream) != hipSuccess)
@@ -905,7 +899,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     ctx->last.cfg = *cfg;
     ctx->last.rgb = false;          // the luma frames are in d_in
     ctx->last.in_place = in_place != nullptr;   // ... or were read in place (not in d_in)
-    ctx->last.in_user = user_out && total <= user_cap;
     return FDF_OK;
 }
 
@@ -913,22 +906,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
 // `out_scores` is given, to the host.
 int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
     if (!n) return FDF_OK;
-    if (ctx->last.in_user) {
-        // the points are only in the buffer of the call that made them: compact them again
-        // from the band slots into h_out
-        int rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points,
-                             (size_t)ctx->last.total, ctx->stream);
-        if (rc) return rc;
-        fdfk::CompactParams c = ctx->last_compact;
-        c.out = ctx->hd_out;
-        c.cap = ctx->h_out_points;
-        c.kp_stats = nullptr;
-        c.group_sums = nullptr;
-        if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
-            hipStreamSynchronize(ctx->stream) != hipSuccess)
-            return FDF_ERR_DEVICE;
-        ctx->last.in_user = false;
-    }
     const LastResult& L = ctx->last;
     if (out_scores && L.in_place) return FDF_ERR_ARG;
     hipError_t e = hipSuccess;
@@ -993,24 +970,8 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
         offs = local.data();
     }
     // unscored calls take the host-mapped output (no copy back); the scored ones keep the
-    // points on the device for the score kernel.  A caller's output buffer in pinned host
-    // memory (all `cap` points in one device-mapped range) is written by the kernels
-    // themselves, with no copy from h_out after the call.
-    uint2* user_out = nullptr;
-    if (!scored && cap) {
-        hipPointerAttribute_t a, z;
-        if (hipPointerGetAttributes(&a, out) == hipSuccess && a.type == hipMemoryTypeHost &&
-            a.devicePointer) {
-            const uint8_t* last = reinterpret_cast<const uint8_t*>(out) + cap * sizeof(fdf_point) - 1;
-            if (hipPointerGetAttributes(&z, last) == hipSuccess && z.type == hipMemoryTypeHost &&
-                static_cast<const uint8_t*>(z.devicePointer) ==
-                    static_cast<const uint8_t*>(a.devicePointer) + (cap * sizeof(fdf_point) - 1))
-                user_out = static_cast<uint2*>(a.devicePointer);
-        }
-        (void)hipGetLastError();       // pageable memory (or a range past the pinning): no error
-    }
-    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored,
-                  user_out, cap);
+    // points on the device for the score kernel
+    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored);
     if (rc) return rc;
     const uint64_t total = offs[n_frames];
     if (total > cap && ctx->last.in_place) {
@@ -1021,10 +982,8 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
             return FDF_ERR_DEVICE;
         ctx->last.in_place = false;
     }
-    if (!ctx->last.in_user) {
-        rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
-        if (rc) return rc;
-    }
+    rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
+    if (rc) return rc;
     *n_out = (size_t)total;
     return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
