@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The latency instances measured here are in commit 3307c16, taken out again: DESIGN.md §7.5.)
 # Round 5 e16: latency instances (fdf_sweep_latency.hip: units leave their last 8-step block
 # at their last row) for grids whose units end inside a block.  The GPU suite on the new
 # library, then single device frames and the batch configurations against the previous build

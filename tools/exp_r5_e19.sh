@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The pinned-output change measured here is in commit 6fd9651, taken out again: DESIGN.md §7.5.)
 # Round 5 e19: points written by the kernels straight into a caller's pinned output buffer
 # (no memcpy from the context's staging after the call): host-path tests, then fdf_detect end
 # to end (pinned frame, pinned output: tools/host_latency.py) against the previous build.
