@@ -663,13 +663,16 @@ def raster_order_ok(pts, offsets, W):
     return bool(np.all(inc))
 
 
-def batch_parity(oracle, copies, bufs, tm, t, n, nms, W):
+def batch_parity(oracle, copies, bufs, tm, t, n, nms, W, redo=None):
     """Whole-batch parity outside the timed region (the reference's
     integration test compares the whole output Vec, tests/compare.rs:45-61): every frame of
     every input copy goes through the CPU checker (oracle.avx2_detect_batch: the AVX2 port of
     src/fast_simd.rs over a thread pool, itself pinned to the scalar oracle by
-    tests/test_oracle.py), and every lane's last result -- offsets and points of all its
-    frames -- must equal its copy's.  The scalar oracle (oracle/fast_oracle.c) also checks the
+    tests/test_oracle.py), and every copy's GPU result -- offsets and points of all its
+    frames -- must equal the checker's: the lanes' last results for the copies they read last,
+    and for every other copy one more call after the timed region (`redo(copy)` -> the lane
+    whose buffers hold it; ADVICE r05: with more copies than lanes the timed region leaves
+    only the last L copies' results).  The scalar oracle (oracle/fast_oracle.c) also checks the
     first, middle and last frame of the last lane's copy directly.  Returns the record and the
     keypoints per timed step (the copies' exact totals weighted by the steps that read them)."""
     ref = {}
@@ -677,33 +680,76 @@ def batch_parity(oracle, copies, bufs, tm, t, n, nms, W):
         ref[c] = oracle.avx2_detect_batch(copies[c], t, n, nms)
     count = copies[0].shape[0]
     ok, order_ok, compared = True, True, []
-    for lane, c in sorted(tm.lane_copy.items()):
+
+    def compare(lane, c, how):
+        nonlocal ok, order_ok
         o = bufs.offs[lane][: count + 1].cpu().numpy().astype(np.uint64)
         total = int(o[-1])
         rp, ro = ref[c]
         if total > bufs.out[lane].shape[0]:
             ok = False
-            continue
+            return
         p = bufs.out[lane][:total].cpu().numpy().astype(np.uint32)
         ok &= bool(np.array_equal(o, ro)) and bool(np.array_equal(p, rp))
         order_ok &= raster_order_ok(p, o, W)
-        compared.append({"lane": lane, "copy": c, "frames": count, "keypoints": total})
+        compared.append({"lane": lane, "copy": c, "frames": count, "keypoints": total,
+                         "result": how})
+
+    for lane, c in sorted(tm.lane_copy.items()):
+        compare(lane, c, "timed")
     c_last = tm.lane_copy.get(tm.last, 0)
     rp, ro = ref[c_last]
     sampled = sorted({0, count // 2, count - 1})
     scalar_ok = all(bool(np.array_equal(rp[ro[f]:ro[f + 1]],
                                          oracle.detect(copies[c_last][f].cpu().numpy(), t, n, nms)))
                     for f in sampled)
+    if redo is not None:
+        for c in sorted(set(range(len(copies))) - set(tm.lane_copy.values())):
+            compare(redo(c), c, "after")
     kp_per_copy = [int(ref[c][1][-1]) for c in range(len(copies))]
     steps = sum(tm.copy_steps.values()) or 1
     kp_step = sum(kp_per_copy[c] * s for c, s in tm.copy_steps.items()) / steps
     rec = {"oracle_frames": "all", "frames_per_copy": count, "copies_checked": len(copies),
+           "copies_compared": len({x["copy"] for x in compared}),
            "lanes_compared": compared, "bit_exact": bool(ok and scalar_ok),
            "gpu_equals_checker_all_frames": bool(ok), "raster_order": order_ok,
            "checker": "oracle.avx2_detect_batch (AVX2 port, pinned to fast_oracle.c)",
            "scalar_oracle_frames": sampled, "scalar_oracle_copy": c_last,
            "scalar_oracle_equal": bool(scalar_ok), "keypoints_per_copy": kp_per_copy}
     return rec, kp_step
+
+
+def redo_on_lane0(lanes, bufs, copies, cfg):
+    """batch_parity's `redo`: copy c once more on lane 0 (synchronised), its result in lane
+    0's buffers."""
+    import torch
+
+    def redo(c):
+        torch.cuda.synchronize()
+        lanes.detect_device(0, copies[c], cfg, bufs.out[0], bufs.offs[0], after_current=False)
+        torch.cuda.synchronize()
+        return 0
+    return redo
+
+
+def shard_leg(fast_hip, workloads, oracle, lanes, cfg, args, world, device, first, count, nms):
+    """One frame-sharded leg: `count` frames per call from global frame `first` on the lanes,
+    distinct copies, whole-batch parity, its own roofline.  Serves config 4's strong split
+    (N > 1) and, at N = 1, the 64-frame shard one GPU of the 8-way split runs (VERDICT r05
+    item 6)."""
+    W, H = args.width, args.height
+    cop = make_batch(workloads, first, count, W, H, device, min_bytes=1 << 29, lanes=args.lanes)
+    buf = LaneBufs(len(lanes), max(count, 1) * 200_000, count, device)
+    t = timed_steps(fast_hip, lanes, buf, cop, cfg, args.steps, args.warmup, world,
+                    settle=args.settle_seconds)
+    e = reduce_max(t.elapsed, world, device)
+    par, kpf = batch_parity(oracle, cop, buf, t, args.threshold, args.count, nms, W,
+                            redo=redo_on_lane0(lanes, buf, cop, cfg))
+    kp = int(round(kpf))
+    in_bytes = count * W * H
+    roof = roofline_of(t, in_bytes + 8 * kp + 4 * count, in_bytes, (None, None))
+    del cop, buf
+    return t, e, par, kp, roof
 
 
 def select_device(ranks_share_device, world, local):
@@ -772,7 +818,7 @@ def main(argv=None):
         kp_step = float(np.mean([int(bufs.offs[i][count].item()) for i in tm.lane_copy]))
     else:
         parity, kp_step = batch_parity(oracle, copies, bufs, tm, args.threshold, args.count,
-                                       nms, W)
+                                       nms, W, redo=redo_on_lane0(lanes, bufs, copies, cfg))
         bad = reduce_sum(0.0 if parity["bit_exact"] else 1.0, world, device)
         parity["ranks"] = {"world": world, "ranks_bit_exact": int(world - bad),
                            "all_ranks_bit_exact": bad == 0,
@@ -808,7 +854,8 @@ def main(argv=None):
                              world, settle=args.settle_seconds)
             e2 = reduce_max(t2.elapsed, world, device)
             par2, kp2f = batch_parity(oracle, copies, bufs, t2, args.threshold, args.count,
-                                      NMS_NAMES[other], W)
+                                      NMS_NAMES[other], W,
+                                      redo=redo_on_lane0(lanes, bufs, copies, ocfg))
             kp2 = int(round(kp2f))
             leg = {"workload": f"same batch, nms={other}",
                    "value": round(pixels / e2 * args.steps / 1e6, 1), "unit": "Mpixels/s",
@@ -840,26 +887,39 @@ def main(argv=None):
         # BASELINE config 4 as defined: 512 frames in total, contiguous shard per GPU (run
         # with --no-extras too: it is the multi-GPU line's own strong-scaling number)
         f4, c4 = strong_shard(rank, world, 512)
-        cop4 = make_batch(workloads, f4, c4, W, H, device, min_bytes=1 << 29, lanes=args.lanes)
-        buf4 = LaneBufs(len(lanes), max(c4, 1) * 200_000, c4, device)
-        t4 = timed_steps(fast_hip, lanes, buf4, cop4, cfg, args.steps, args.warmup, world,
-                         settle=args.settle_seconds)
-        e4 = reduce_max(t4.elapsed, world, device)
-        par4, kp4f = batch_parity(oracle, cop4, buf4, t4, args.threshold, args.count, nms, W)
-        kp4 = int(reduce_sum(float(round(kp4f)), world, device))
+        t4, e4, par4, kp4r, roof4 = shard_leg(fast_hip, workloads, oracle, lanes, cfg, args,
+                                              world, device, f4, c4, nms)
+        kp4 = int(reduce_sum(float(kp4r), world, device))
         bad4 = reduce_sum(0.0 if par4["bit_exact"] else 1.0, world, device)
         extras["config4_strong"] = {
             "workload": f"512 {W}x{H} frames in total, {c4} per GPU (rank {rank}), "
-                        f"nms={args.nms}; rotated through {len(cop4)} distinct copies (HBM reads)",
+                        f"nms={args.nms}; distinct copies per lane (HBM reads)",
             "value": round(512 * W * H / e4 * args.steps / 1e6, 1), "unit": "Mpixels/s",
             "ms_per_step": round(e4 * 1e3 / args.steps, 4), "scaling": "strong",
             "frames_total": 512, "keypoints_per_step": kp4,
             "lanes": t4.lanes,
             "kernel_ms_avg": round(t4.span_ms / t4.steps, 4),
             "launch_ms_avg": round(float(np.mean(t4.det)), 4) if len(t4.det) else None,
+            "roofline_rank0": roof4,
             "parity": {"oracle_frames": "all", "all_ranks_bit_exact": bad4 == 0,
                        "rank0": par4}}
-        del cop4, buf4
+    if world == 1 and not strong and not args.no_extras and not args.no_strong_leg:
+        # the per-GPU shard of config 4 split over 8 GPUs (64 frames per call), on this one
+        # GPU: the measured basis of the 8-way strong-scaling projection
+        c64 = max(1, 512 // 8)
+        t6, e6, par6, kp6, roof6 = shard_leg(fast_hip, workloads, oracle, lanes, cfg, args,
+                                             world, device, 0, c64, nms)
+        ms64 = e6 * 1e3 / args.steps
+        extras["shard64"] = {
+            "workload": f"{c64} {W}x{H} frames per call (config 4's per-GPU shard at 8 GPUs), "
+                        f"nms={args.nms}, {t6.lanes} lanes, distinct copies",
+            "value": round(c64 * W * H / e6 * args.steps / 1e6, 1), "unit": "Mpixels/s",
+            "ms_per_step": round(ms64, 4), "keypoints_per_step": kp6,
+            "roofline": roof6, "parity": par6,
+            # 8 GPUs each running this shard against one GPU's 512-frame step / 8
+            "projected_8gpu_strong_efficiency": round(ms_per_step / 8 / ms64, 4),
+            "projection_basis": "headline ms_per_step / 8 over this leg's ms_per_step; "
+                                "the 8-GPU curve itself is unmeasured on hardware"}
     if rank == 0 and not args.no_extras:
         # single-frame latency (device-resident frame, one launch, HIP events), on --input
         # when given (the reference's bench image, benches/benchmark.rs:6-16), else S1 frame 0

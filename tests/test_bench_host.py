@@ -123,3 +123,49 @@ def test_batch_parity_checks_every_frame():
     bad = bufs_from(ref)
     bad.offs[0][2] += 1
     assert not bench.batch_parity(oracle, copies, bad, tm, 16, 9, 1, W)[0]["bit_exact"]
+
+
+def test_batch_parity_compares_copies_no_lane_read_last():
+    """with more copies than lanes, the copies the lanes did not read last are
+    detected once more (`redo`) and compared too; a wrong result there fails the record."""
+    import numpy as np
+    import torch
+
+    import workloads
+    from oracle import oracle
+
+    W, H, F = 160, 90, 3
+    copies = [torch.from_numpy(np.stack([workloads.s1_frame(i + 211 * c, W, H) for i in range(F)]))
+              for c in range(4)]
+    ref = [oracle.avx2_detect_batch(c, 16, 9, 1) for c in copies]
+
+    class Bufs:
+        pass
+
+    def put(b, lane, r):
+        p, o = r
+        b.out[lane] = torch.from_numpy(np.concatenate([p.astype(np.int32), np.zeros((7, 2), np.int32)]))
+        b.offs[lane] = torch.from_numpy(o.astype(np.int64))
+
+    def run(corrupt_copy=None):
+        b = Bufs()
+        b.out, b.offs = [None, None], [None, None]
+        put(b, 0, ref[2])
+        put(b, 1, ref[3])
+        redone = []
+
+        def redo(c):
+            put(b, 0, ref[c])
+            if c == corrupt_copy:
+                b.out[0][0, 0] += 1
+            redone.append(c)
+            return 0
+        tm = bench.Timed(0.01, 1.0, [], [], 1, 4, 2, lane_copy={0: 2, 1: 3},
+                         copy_steps={0: 1, 1: 1, 2: 1, 3: 1})
+        rec, _ = bench.batch_parity(oracle, copies, b, tm, 16, 9, 1, W, redo=redo)
+        return rec, redone
+
+    rec, redone = run()
+    assert rec["bit_exact"] and rec["copies_compared"] == 4 and redone == [0, 1]
+    assert [c["result"] for c in rec["lanes_compared"]] == ["timed", "timed", "after", "after"]
+    assert not run(corrupt_copy=1)[0]["bit_exact"]

@@ -1,0 +1,45 @@
+#!/bin/bash
+# Round-6 experiments, one function each; run on the GPU box as
+#   bash tools/exp_r6.sh <id>
+# Each writes under gpurun_out/r6_<id>/; the committed results are in profiles/r06/.
+set -e
+cd "$GRAFT_REPO_ROOT"
+
+C5="--width 3840 --height 2160 --frames 128 --threshold 8 --count 12 --nms sad"
+
+# config 5's one-lane regression (0.643 -> 0.71 ms when every lane got its
+# own input copy).  Interleaved A/B of (lanes, copies) = (1,1) (1,3) (3,1) (3,3): ms per step
+# and per-launch durations, then FETCH_SIZE and TCC hit/miss passes for each (own rocprofv3
+# run per counter set, nothing else traced).
+exp_c5ab() {
+  O=gpurun_out/r6_c5ab
+  mkdir -p $O
+  : > $O/ab.jsonl
+  for r in 1 2 3; do
+    for lc in "1 1" "1 3" "3 1" "3 3"; do
+      set -- $lc
+      timeout -k 10 150 python3 bench.py $C5 --lanes $1 --copies $2 --no-extras --no-parity \
+          --cpu-seconds 0 --steps 30 --warmup 5 > $O/run.json 2> $O/run.err
+      python3 -c "import json,sys; d=json.load(open('$O/run.json')); r=d['roofline']; print(json.dumps({'round': $r, 'lanes': $1, 'copies': $2, 'ms_per_step': d['ms_per_step'], 'kernel_ms_avg': r['kernel_ms_avg'], 'launch_ms_avg': r['launch_ms_avg']}))" >> $O/ab.jsonl
+    done
+  done
+  cat $O/ab.jsonl
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  SHORT="--no-extras --no-parity --cpu-seconds 0 --steps 6 --warmup 1 --settle-seconds 0"
+  for lc in "1 1" "1 3" "3 1" "3 3"; do
+    set -- $lc
+    T=l$1_c$2
+    timeout -k 10 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$T -o p -- \
+        python3 bench.py $C5 $SHORT --lanes $1 --copies $2 > $O/fetch_$T.json 2> $O/fetch_$T.log
+    timeout -k 10 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/tcc_$T -o p -- \
+        python3 bench.py $C5 $SHORT --lanes $1 --copies $2 > $O/tcc_$T.json 2> $O/tcc_$T.log
+    python3 tools/pmc_summary.py $O/fetch_$T $O/tcc_$T > $O/pmc_$T.json
+    rm -rf $O/fetch_$T $O/tcc_$T
+  done
+  echo c5ab done
+}
+
+case "${1:-}" in
+  c5ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab}" >&2; exit 2 ;;
+esac
