@@ -21,6 +21,9 @@ $(CSRC)/fdf_kernels.o: $(CSRC)/fdf_kernels.hip $(CSRC)/fdf_compact.h $(CSRC)/fdf
 $(CSRC)/fdf_sweep.o: $(CSRC)/fdf_sweep.hip $(CSRC)/fdf_sweep_impl.h $(CSRC)/fdf_compact.h $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(CSRC)/fdf_sweep_latency.o: $(CSRC)/fdf_sweep_latency.hip $(CSRC)/fdf_sweep_impl.h $(CSRC)/fdf_compact.h $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(CSRC)/fdf_sweep_rgb.o: $(CSRC)/fdf_sweep_rgb.hip $(CSRC)/fdf_sweep_impl.h $(CSRC)/fdf_compact.h $(CSRC)/fdf_kernels.h $(CSRC)/fdf_common.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -30,7 +33,7 @@ $(CSRC)/fdf_api.o: $(CSRC)/fdf_api.cpp $(CSRC)/fdf_kernels.h include/fdf.h
 $(CSRC)/fdf_pipeline.o: $(CSRC)/fdf_pipeline.cpp include/fdf.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_sweep_rgb.o $(CSRC)/fdf_api.o $(CSRC)/fdf_pipeline.o
+$(LIBFDF): $(CSRC)/fdf_kernels.o $(CSRC)/fdf_sweep.o $(CSRC)/fdf_sweep_latency.o $(CSRC)/fdf_sweep_rgb.o $(CSRC)/fdf_api.o $(CSRC)/fdf_pipeline.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle/liboracle.so: oracle/fast_oracle.c oracle/fast_oracle.h

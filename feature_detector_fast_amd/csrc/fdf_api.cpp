@@ -32,6 +32,8 @@ struct LastResult {
     bool rgb = false;              // frames in d_rgb (RGB8); scores need their luma in d_in
     bool in_place = false;         // the frame was read in place from pinned host memory: not
                                    // in d_in, so the result has no scores (fdf_fetch_last)
+    bool in_user = false;          // the points went straight into the caller's pinned buffer
+                                   // (not h_out: fdf_fetch_last compacts them again)
     // fdf_detect_batch_multi: the call's generation (0: not a multi-context result) and this
     // context's shard of it, checked by fdf_fetch_last_multi
     uint64_t multi_gen = 0;
@@ -98,6 +100,11 @@ struct fdf_ctx {
     hipEvent_t done = nullptr;
     hipStream_t done_stream = nullptr;
     bool done_valid = false;
+    // the last enqueue's work is on done_stream but `done` is not recorded after it yet: on
+    // the context's own stream and the null stream (streams that outlive every call) the
+    // record waits until something needs it (another stream's call, a host wait), so a
+    // stream of back-to-back calls enqueues one packet per call, not two
+    bool done_pending = false;
     // the last enqueue's compaction, relaunched when the host output has to grow
     fdfk::CompactParams last_compact{};
     LastResult last;
@@ -169,9 +176,31 @@ int check_shape(uint32_t w, uint32_t h, int* empty) {
     return FDF_OK;
 }
 
+// `done` covers the last enqueue's work (recorded now if that was deferred).
+hipError_t record_done(fdf_ctx* ctx) {
+    if (!ctx->done_valid || !ctx->done_pending) return hipSuccess;
+    ctx->done_pending = false;
+    return hipEventRecord(ctx->done, ctx->done_stream);
+}
+
+// After enqueueing the context's work on `stream`: `done` is to follow it, now or (streams
+// that outlive every call: the context's own, the null stream) when first needed.
+hipError_t note_done(fdf_ctx* ctx, hipStream_t stream) {
+    ctx->done_stream = stream;
+    ctx->done_valid = true;
+    ctx->done_pending = true;
+    if (stream == ctx->stream || stream == nullptr) return hipSuccess;
+    return record_done(ctx);
+}
+
 // The device work of the last enqueue (whatever stream it ran on) has finished.
 void wait_done(fdf_ctx* ctx) {
-    if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
+    if (!ctx->done_valid) return;
+    if (record_done(ctx) != hipSuccess) {
+        (void)hipStreamSynchronize(ctx->done_stream);
+        return;
+    }
+    (void)hipEventSynchronize(ctx->done);
 }
 
 // Grow a workspace buffer to `need` elements (+1/8 headroom).  The old buffer may still be
@@ -249,7 +278,7 @@ Geometry pick_geometry(uint32_t n_frames, uint32_t w, uint32_t h, uint32_t nms,
     // LDS per workgroup sets the workgroups per CU: <= 40 KB keeps 4.
     // Without NMS a 35 KB budget (bands of ~122 rows at 1080p) measured faster than the
     // tallest band that fits (more, shorter workgroups: a shorter grid tail).
-    uint32_t budget = (nms ? 40000u : 35000u) + 4 * fdfk::kWinBytes;
+    uint32_t budget = (nms ? 40000u : 35000u);
 #ifdef FDF_DEBUG_BUILD
     if (const char* b = std::getenv("FDF_LDS_BUDGET"))
         budget = std::min<uint32_t>(fdfk::kSweepMaxLds, (uint32_t)std::strtoul(b, nullptr, 0));
@@ -343,12 +372,14 @@ volatile uint32_t* lookback_error_word(fdf_ctx* ctx) {
 }
 
 // Takes (reads and clears) the look-back error word: bit 0 a direct-output band's look-back
-// ran out, bit 1 a band's wait for its upload chunk.
+// ran out, bit 1 a band's wait for its upload chunk, bit 2 a workgroup's start ticket lay
+// past its grid (the device counter and ticket_next disagree: both are reset).
 uint32_t take_lookback_error(fdf_ctx* ctx) {
     volatile uint32_t* e = lookback_error_word(ctx);
     if (!e || *e == 0) return 0;
     const uint32_t v = *e;
     *e = 0;
+    if (v & 4u) ctx->sums_dirty = true;
     return v;
 }
 
@@ -428,7 +459,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     }
     // workgroup slots of the device: 4 per CU (4 waves per SIMD); fdf_ctx_set_geometry's
     // min_tasks replaces it (1: the tall bands of a large batch for any job)
-    const uint64_t per_cu = fdfk::kWinBytes ? 2ull : 4ull;    // FDF_LDS_WINDOW: 2 per CU
+    const uint64_t per_cu = 4;
     const uint64_t slots = ctx->min_tasks ? ctx->min_tasks
                                           : (ctx->cus ? per_cu * ctx->cus : kDefaultMinTasks);
     const Geometry geo = pick_geometry(n_frames, w, h, cfg->nms, slots, density, ctx->band_rows,
@@ -465,7 +496,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         return FDF_ERR_DEVICE;
     }
     if (ctx->done_valid && ctx->done_stream != stream &&
-        hipStreamWaitEvent(stream, ctx->done, 0) != hipSuccess)
+        (record_done(ctx) != hipSuccess || hipStreamWaitEvent(stream, ctx->done, 0) != hipSuccess))
         return FDF_ERR_DEVICE;
     int rc;
     if ((rc = ensure(ctx, &ctx->d_slots, &ctx->slots_bytes, (size_t)(ntasks * slot_bytes), stream))) return rc;
@@ -600,10 +631,18 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         }
         ev = &ctx->ev[4 * ctx->timed];
     }
-    if ((rgb ? fdfk::launch_sweep_rgb(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr,
-                                      ev ? ev[1] : nullptr)
-             : fdfk::launch_sweep(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr,
-                                  ev ? ev[1] : nullptr)) != hipSuccess) {
+    // a small grid whose units are shorter than one 8-step block (a single frame's latency
+    // bands) runs the instances that leave the block at the unit's last row
+    // (fdf_sweep_latency.hip; 1080p NMS off 13.5 -> 12.5 us, max-t 17.3 -> 17.0 us per frame).
+    // Long units keep whole blocks: the exit tests cost the batch loop more than the padding
+    // steps they save (512 x 1080p NMS off, 61-row units: +0.6 %, profiles/r05/e16_*)
+    const uint32_t unit_steps = (R + geo.nsub - 1) / geo.nsub +
+                                fdfk::band_halo(cfg->nms) * (geo.nsub == 1 ? 2u : 1u);
+    const bool exit_in_block = !rgb && direct && unit_steps < fdfk::kSweepRing;
+    auto launch = rgb ? fdfk::launch_sweep_rgb
+                      : (exit_in_block ? fdfk::launch_sweep_latency : fdfk::launch_sweep);
+    if (launch(p, cfg->nms, cfg->count, stream, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr) !=
+        hipSuccess) {
         ctx->sums_dirty = true;
         return FDF_ERR_DEVICE;
     }
@@ -620,9 +659,7 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         ++ctx->timed;
     }
     ctx->last_compact = c;
-    if (hipEventRecord(ctx->done, stream) != hipSuccess) return FDF_ERR_DEVICE;
-    ctx->done_stream = stream;
-    ctx->done_valid = true;
+    if (note_done(ctx, stream) != hipSuccess) return FDF_ERR_DEVICE;
     return FDF_OK;
 }
 
@@ -661,7 +698,7 @@ int check_host_args(const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t
 // with image 0.24.6's to_luma8 before detection (src/main.rs:58).
 int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
              size_t row_stride, size_t frame_stride, const fdf_config* cfg, bool rgb,
-             uint64_t* offs, bool host_out) {
+             uint64_t* offs, bool host_out, uint2* user_out = nullptr, size_t user_cap = 0) {
     ctx->last = LastResult{};          // invalid, and not a shard of a multi-context call
     const size_t frame_bytes = (size_t)w * h;
     const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
@@ -681,6 +718,10 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         out_dev = ctx->hd_out;
         offs_dev = ctx->hd_offs;
         out_cap = &ctx->h_out_points;
+        if (user_out) {                // the caller's pinned buffer, written by the kernels
+            out_dev = user_out;
+            out_cap = &user_cap;
+        }
     } else {
         if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, guess, ctx->stream))) return rc;
         if ((rc = ensure(ctx, &ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, ctx->stream)))
@@ -847,6 +888,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     };
     if (fetch_offsets() != hipSuccess) return FDF_ERR_DEVICE;
     if (const uint32_t err = take_lookback_error(ctx)) {
+        if (err & 4u) return FDF_ERR_DEVICE;   // a band never ran: nothing to rebuild from
         if (err & 2u) {
             // a band's wait for its upload chunk ran out (the copies are drained now): detect
             // again from the whole frame, uploaded before the launch
@@ -881,12 +923,11 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, (size_t)total, ctx->stream))) return rc;
             c.out = ctx->d_out;
         }
-        c.cap = *out_cap;
+        c.cap = host_out ? ctx->h_out_points : ctx->out_points;
         c.kp_stats = nullptr;           // already reported (and reset) by the first compaction
         if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
-            hipEventRecord(ctx->done, ctx->stream) != hipSuccess)
+            note_done(ctx, ctx->stream) != hipSuccess)
             return FDF_ERR_DEVICE;
-        ctx->done_stream = ctx->stream;
         // the host reads h_out next: the compaction must be done
         if (host_out && hipStreamSynchronize(ctx->stream) != hipSuccess) return FDF_ERR_DEVICE;
     }
@@ -899,6 +940,34 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     ctx->last.cfg = *cfg;
     ctx->last.rgb = false;          // the luma frames are in d_in
     ctx->last.in_place = in_place != nullptr;   // ... or were read in place (not in d_in)
+    ctx->last.in_user = user_out && total <= user_cap;
+    return FDF_OK;
+}
+
+// A host result whose points went straight into the caller's pinned buffer (LastResult::
+// in_user) exists only there: compact it again from the band slots into h_out (lock held).
+// Called before anything reads it back (fdf_fetch_last) and before a device call reuses the
+// slots and replaces last_compact.
+int settle_user_points(fdf_ctx* ctx) {
+    if (!ctx->last.valid || !ctx->last.in_user) return FDF_OK;
+    ctx->last.in_user = false;
+    if (ctx->last.total == 0) return FDF_OK;
+    int rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points,
+                         (size_t)ctx->last.total, ctx->stream);
+    if (rc) {
+        ctx->last.valid = false;
+        return rc;
+    }
+    fdfk::CompactParams c = ctx->last_compact;
+    c.out = ctx->hd_out;
+    c.cap = ctx->h_out_points;
+    c.kp_stats = nullptr;
+    c.group_sums = nullptr;
+    if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        ctx->last.valid = false;
+        return FDF_ERR_DEVICE;
+    }
     return FDF_OK;
 }
 
@@ -906,6 +975,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
 // `out_scores` is given, to the host.
 int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
     if (!n) return FDF_OK;
+    if (int rc = settle_user_points(ctx)) return rc;
     const LastResult& L = ctx->last;
     if (out_scores && L.in_place) return FDF_ERR_ARG;
     hipError_t e = hipSuccess;
@@ -970,8 +1040,24 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
         offs = local.data();
     }
     // unscored calls take the host-mapped output (no copy back); the scored ones keep the
-    // points on the device for the score kernel
-    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored);
+    // points on the device for the score kernel.  A caller's output buffer in pinned host
+    // memory (all `cap` points in one device-mapped range) is written by the kernels
+    // themselves, with no copy from h_out after the call.
+    uint2* user_out = nullptr;
+    if (!scored && cap) {
+        hipPointerAttribute_t a, z;
+        if (hipPointerGetAttributes(&a, out) == hipSuccess && a.type == hipMemoryTypeHost &&
+            a.devicePointer) {
+            const uint8_t* last = reinterpret_cast<const uint8_t*>(out) + cap * sizeof(fdf_point) - 1;
+            if (hipPointerGetAttributes(&z, last) == hipSuccess && z.type == hipMemoryTypeHost &&
+                static_cast<const uint8_t*>(z.devicePointer) ==
+                    static_cast<const uint8_t*>(a.devicePointer) + (cap * sizeof(fdf_point) - 1))
+                user_out = static_cast<uint2*>(a.devicePointer);
+        }
+        (void)hipGetLastError();       // pageable memory (or a range past the pinning): no error
+    }
+    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored,
+                  user_out, cap);
     if (rc) return rc;
     const uint64_t total = offs[n_frames];
     if (total > cap && ctx->last.in_place) {
@@ -982,8 +1068,10 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
             return FDF_ERR_DEVICE;
         ctx->last.in_place = false;
     }
-    rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
-    if (rc) return rc;
+    if (!ctx->last.in_user) {
+        rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
+        if (rc) return rc;
+    }
     *n_out = (size_t)total;
     return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
@@ -1301,6 +1389,8 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
                    ? FDF_OK
                    : FDF_ERR_DEVICE;
     }
+    // the slots and last_compact are about to be reused
+    if (int rs = settle_user_points(ctx)) return rs;
     return enqueue(ctx, d_frames, n_frames, width, height,
                    n_frames > 1 ? frame_stride_bytes : (uint64_t)width * height, cfg,
                    reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s);
@@ -1337,6 +1427,8 @@ int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_fram
                    ? FDF_OK
                    : FDF_ERR_DEVICE;
     }
+    // the slots and last_compact are about to be reused
+    if (int rs = settle_user_points(ctx)) return rs;
     return enqueue(ctx, d_frames, n_frames, width, height, n_frames > 1 ? frame_stride_bytes : fb,
                    cfg, reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s, true);
 }

@@ -90,21 +90,8 @@ constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix bl
 static_assert(kScoreListCap * 2 <= 4 * kSweepPixelQ * 4, "ranked scores must fit the FIFO area");
 static_assert(kScoreListCap % 256 == 0, "the spill NMS pass holds the list 1/256 per thread");
 static_assert(kScoreListCap < 4096, "the LDS NMS pass keeps rank + 1 in a list entry's 12 score bits");
-// A/B variant (FDF_LDS_WINDOW, variant builds only): each wave keeps the
-// last kWinRows pixel rows it streamed in an LDS ring (64 lanes x 16 bytes per row), a batch's
-// 7x7 windows are read from there instead of gathered from L2/HBM, and every queued candidate
-// is issued within 3 rows so its rows are still in the ring.  40 KB more per workgroup: 2
-// workgroups per CU (2 waves per SIMD) instead of 4.
-#if defined(FDF_LDS_WINDOW) || defined(FDF_LDS_PAD)
-// (FDF_LDS_PAD: the same LDS reserved but unused -- the occupancy cost alone, for the A/B)
-constexpr uint32_t kWinRows = 10;
-constexpr uint32_t kWinBytes = kWinRows * 1024;   // per wave
-#else
-constexpr uint32_t kWinBytes = 0;
-#endif
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
-    uint32_t win;                // FDF_LDS_WINDOW: 4 per-wave row rings of kWinBytes
     uint32_t seltab;             // during the sweep: the 256-entry set-bit table (1 KB) in
                                  // the rank-prefix area, which NMS uses only after the sweep
     uint32_t nms_area_entries;   // u16 ranked scores that fit [pq, bprefix) after the sweep
@@ -128,8 +115,7 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     L.seltab = L.bprefix;
     const uint32_t prefix_end = L.rprefix + (nms ? align16(rows * 4) : 0u);
     L.misc = prefix_end > L.seltab + 1024u ? prefix_end : L.seltab + 1024u;
-    L.win = L.misc + 64;
-    L.total = L.win + 4 * kWinBytes;
+    L.total = L.misc + 64;
     return L;
 }
 
@@ -245,6 +231,10 @@ hipError_t launch_compact(const CompactParams& c, hipStream_t stream, hipEvent_t
                           hipEvent_t stop = nullptr);
 hipError_t launch_sweep(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
                         hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// The same detector whose units leave their last 8-step block at their last row
+// (fdf_sweep_latency.hip): for grids of short units (a single frame's latency bands)
+hipError_t launch_sweep_latency(const BandParams& p, uint32_t nms, uint32_t n, hipStream_t stream,
+                                hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // Workgroups of the detector instance (nms, n; grey or RGB) one CU holds at once with
 // `lds_bytes` of dynamic LDS (the runtime's occupancy calculator: registers, LDS, waves).
 hipError_t sweep_occupancy(uint32_t nms, uint32_t n, uint32_t lds_bytes, bool rgb, int* wg_per_cu);

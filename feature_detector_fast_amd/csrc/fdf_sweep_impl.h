@@ -1,7 +1,9 @@
 // fdf_sweep_impl.h -- column-sweep FAST-9..16 kernel for MI355X (gfx950), the production path.
-// Included by fdf_sweep.hip (grey frames: FDF_SWEEP_RGB 0, namespace fdfk::grey) and
-// fdf_sweep_rgb.hip (RGB8 frames converted to luma in the row and window loads:
-// FDF_SWEEP_RGB 1, namespace fdfk::rgb); each translation unit instantiates its 24 kernels.
+// Included by fdf_sweep.hip (grey frames: FDF_SWEEP_RGB 0, namespace fdfk::grey),
+// fdf_sweep_latency.hip (grey frames, units leave their last 8-step block early: namespace
+// fdfk::grey_lat) and fdf_sweep_rgb.hip (RGB8 frames converted to luma in the row and window
+// loads: FDF_SWEEP_RGB 1, namespace fdfk::rgb); each translation unit instantiates its 24
+// kernels.
 //
 // Replaces detect<NONMAX>() (iwanders/feature_detector_fast src/fast_simd.rs:301-620) with
 // determine_keypoint (:115-297) and the NMS score functions (:623-718, :722-749).
@@ -62,6 +64,14 @@ constexpr bool kRgb = FDF_SWEEP_RGB != 0;
 #endif
 constexpr int kRing = FDF_SWEEP_TU_RING;
 constexpr int kWavesEU = FDF_SWEEP_TU_WAVES;
+// Units that end inside an 8-step block leave it at their last row (FDF_SWEEP_TU_EXIT, the
+// latency instances of fdf_sweep_latency.hip: a single frame's 3-row units skip 4 padding
+// steps).  The exit tests perturb the long-unit loop's code (512 x 1080p max-t +0.5..+2 %,
+// DESIGN.md §7.6), so the throughput instances keep whole blocks.
+#ifndef FDF_SWEEP_TU_EXIT
+#define FDF_SWEEP_TU_EXIT 0
+#endif
+constexpr bool kExitInBlock = FDF_SWEEP_TU_EXIT != 0;
 constexpr int kPx = kRgb ? 3 : 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -199,7 +209,6 @@ struct SweepShared {
     uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
     const uint32_t* seltab;  // select_bit's table (SweepLayout::seltab)
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
-    uint8_t* win;          // FDF_LDS_WINDOW: this wave's ring of kWinRows pixel rows
 };
 
 struct UnitCtx {
@@ -326,30 +335,6 @@ __device__ __forceinline__ FifoPeek fifo_peek(const SweepShared& sh, const UnitC
     return f;
 }
 
-#ifdef FDF_LDS_WINDOW
-// The 7 row windows of centre (strip column cl, unit row rr + 3) from the wave's LDS ring: ring
-// row (rel % kWinRows) holds unit-relative row rel = row - (ys - 3), 64 lanes x 16 bytes, byte
-// cl = strip column cl.  Rows rr .. rr + 6 wrap at most once.  Unaligned 32-bit LDS reads.
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t* p) {
-    return *reinterpret_cast<const uint32_t*>(p);
-}
-__device__ __forceinline__ void load_ring_windows_lds(Batch& b, const uint8_t* win, uint32_t rr,
-                                                      uint32_t cl) {
-    const uint32_t s0 = rr - kWinRows * ((rr * 6554u) >> 16);   // rr % 10 for rr < 2^14
-    const uint8_t* base = win + s0 * 1024u + cl;
-    const uint8_t* wrap = base - kWinRows * 1024u;
-    const uint32_t k = kWinRows - s0;                            // first row that wraps
-    auto row = [&](uint32_t d) { return (d < k ? base : wrap) + d * 1024u; };
-    b.a0 = lds_u32(row(0) - 1);
-    b.a1 = u32x2{lds_u32(row(1) - 2), lds_u32(row(1) + 2)};
-    b.a2 = u32x2{lds_u32(row(2) - 3), lds_u32(row(2) + 1)};
-    b.a3 = u32x2{lds_u32(row(3) - 3), lds_u32(row(3) + 1)};
-    b.a4 = u32x2{lds_u32(row(4) - 3), lds_u32(row(4) + 1)};
-    b.a5 = u32x2{lds_u32(row(5) - 2), lds_u32(row(5) + 2)};
-    b.a6 = lds_u32(row(6) - 1);
-}
-#endif
-
 template <int LC>
 __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, bool force,
                                              const FifoPeek& pk) {
@@ -360,7 +345,6 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
     b.code = 0;
     const int W = (int)u.src.W;
     int o = 3;                                        // pixel (x, y - 3) of centre (3, 3)
-    uint32_t wrr = 0, wcl = 16;                       // FDF_LDS_WINDOW: ring row, strip column
     const uint32_t nent = pk.nent;
     if (nent != 0) {
         const uint32_t lane = u.lane;
@@ -411,20 +395,10 @@ __device__ __forceinline__ Batch issue_batch(const SweepShared& sh, UnitCtx& u, 
                 b.code = ((uint32_t)(u.ys + (int)(sc >> 10)) << 10) | (sc & 1023u);
                 // rows relative to the unit (< 2^10) times W (< 2^16): a 24-bit multiply
                 o = u.rowbase + (int)__umul24(sc >> 10, (uint32_t)W) + u.S - LC + (int)(sc & 1023u);
-                wrr = sc >> 10;
-                wcl = sc & 1023u;
             }
         }
     }
-#ifdef FDF_LDS_WINDOW
-    (void)o;
-    // the ring rows other lanes wrote this step (see the staging fence above)
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    load_ring_windows_lds(b, sh.win, wrr, wcl);
-#else
-    (void)wrr; (void)wcl;
     load_ring_windows(b, u.src.rs, o, W);
-#endif
     return b;
 }
 
@@ -622,24 +596,6 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
     inflight[QL] = false;
 }
 
-// A/B variant (FDF_MAX_AGE > 0, off in the product): issue a partial
-// batch once the oldest queued candidate is FDF_MAX_AGE rows old, so its gathers read rows the
-// wave streamed recently enough to still be in L2.  `step` is the unit-relative row being
-// swept; the FIFO head entry's code holds its row (spread_code((row - ys) << 6 | lane)).
-#ifndef FDF_MAX_AGE
-#define FDF_MAX_AGE 0
-#endif
-__device__ __forceinline__ bool issue_aged(const SweepShared& sh, const UnitCtx& u, int step) {
-    if constexpr (FDF_MAX_AGE > 0) {
-        if (u.tail == u.head) return false;
-        const uint32_t e0 = __builtin_amdgcn_readfirstlane(sh.pq[u.head & (kSweepPixelQ - 1)]);
-        const int row = (int)(pack_nibbles(e0 & ~kFlagNibbles) >> 6);
-        return step - row >= FDF_MAX_AGE;
-    }
-    (void)sh; (void)u; (void)step;
-    return false;
-}
-
 template <int NMS, int N, bool EXACT>
 __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     constexpr int LC = kLaneCols;
@@ -691,18 +647,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     for (int k = 0; k < 3; ++k) up[k] = load_row<LC, EXACT>(u.src, ys - 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
-#ifdef FDF_LDS_WINDOW
-    // the ring of the last kWinRows rows: unit row rel = row - (ys - 3) in ring row rel % 10;
-    // the prologue's rows ys - 3 .. ys + 2 first, then each step writes its row yv + 3
-    const uint32_t lane16 = lane * 16u;
-    auto win_put = [&](uint32_t rel, const RowV& v) {
-        *reinterpret_cast<RowV*>(sh.win + (rel % kWinRows) * 1024u + lane16) = v;
-    };
-#pragma unroll
-    for (int k = 0; k < 3; ++k) win_put((uint32_t)k, up[k]);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) win_put((uint32_t)(k + 3), Rw[k]);
-#endif
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 #pragma unroll
     for (int k = 0; k < 3; ++k) V[k + 1] = compare_rows<LC>(Rw[k], ~up[k], lk);
@@ -718,7 +662,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
         V[(J) & 3] = compare_rows<LC>(s, nc, lk);                                            \
-        FDF_WIN_PUT(i0 + (J) + 6, s);                                                        \
         const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
         {                                                                                    \
             RowV e;                                                                          \
@@ -781,7 +724,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 else evaluate_batch<NMS, N, LC>(sh, u, lk, issue_batch<LC>(sh, u, true));    \
             }                                                                                \
         }                                                                                    \
-        if (((J) % kIssue) == kIssue - 1 || (kWindowed && (J) == K - 1)) {                   \
+        if (((J) % kIssue) == kIssue - 1) {                                                  \
             /* the batch of this slot is due; issue the next full one into it */             \
             constexpr int q = ((J) / kIssue) % kSweepBatchSlots;                             \
             if (inflight[q]) {                                                               \
@@ -789,58 +732,44 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
                 inflight[q] = false;                                                         \
             }                                                                                \
             if (ablation_flags(u.flags) & kFlagNoFullTest) u.head = u.tail;                                  \
-            if constexpr (kWindowed) {                                                       \
-                /* LDS window: every queued candidate goes now (its rows leave the ring */   \
-                /* soon); all but the last batch are tested at once */                       \
-                Batch nb = issue_batch<LC>(sh, u, true);                                     \
-                while (u.tail != u.head) {                                                   \
-                    evaluate_batch<NMS, N, LC>(sh, u, lk, nb);                               \
-                    nb = issue_batch<LC>(sh, u, true);                                       \
-                }                                                                            \
-                batch[q] = nb;                                                               \
-            } else {                                                                         \
-                batch[q] = issue_batch<LC>(sh, u, issue_aged(sh, u, i0 + (J)));              \
-            }                                                                                \
+            batch[q] = issue_batch<LC>(sh, u, false);                                        \
             inflight[q] = batch[q].n != 0;                                                   \
         }                                                                                    \
     }
 
     static_assert(K == 8 || K == 16, "ring of 8 or 16 rows (a power of two: row codes OR together)");
-#ifdef FDF_LDS_WINDOW
-    constexpr bool kWindowed = true;
-#define FDF_WIN_PUT(rel, v) win_put((uint32_t)(rel), v)
-#else
-    constexpr bool kWindowed = false;
-#define FDF_WIN_PUT(rel, v)
-#endif
     static_assert((K / kIssue) % kSweepBatchSlots == 0 || kSweepBatchSlots == 1,
                   "issue points per loop body must cycle through the batch slots");
     for (int i0 = 0; i0 < T; i0 += K) {
         // FIFO code of row ys + i0 + J: i0 is a multiple of K, so its spread ORs with J's
         const uint32_t lane_row_code = lane_code | spread_code((uint32_t)i0 << 6);
-        FDF_SWEEP_STEP(0)
-        FDF_SWEEP_STEP(1)
-        FDF_SWEEP_STEP(2)
-        FDF_SWEEP_STEP(3)
-        FDF_SWEEP_STEP(4)
-        FDF_SWEEP_STEP(5)
-        FDF_SWEEP_STEP(6)
+        // (latency instances: leave the block after the unit's last row, wave-uniform)
+#define FDF_STEP_EXIT(J) if constexpr (kExitInBlock) { if (i0 + (J) + 1 >= T) break; }
+        FDF_SWEEP_STEP(0) FDF_STEP_EXIT(0)
+        FDF_SWEEP_STEP(1) FDF_STEP_EXIT(1)
+        FDF_SWEEP_STEP(2) FDF_STEP_EXIT(2)
+        FDF_SWEEP_STEP(3) FDF_STEP_EXIT(3)
+        FDF_SWEEP_STEP(4) FDF_STEP_EXIT(4)
+        FDF_SWEEP_STEP(5) FDF_STEP_EXIT(5)
+        FDF_SWEEP_STEP(6) FDF_STEP_EXIT(6)
         FDF_SWEEP_STEP(7)
         if constexpr (K >= 12) {
-            FDF_SWEEP_STEP(8)
-            FDF_SWEEP_STEP(9)
-            FDF_SWEEP_STEP(10)
+            FDF_STEP_EXIT(7)
+            FDF_SWEEP_STEP(8) FDF_STEP_EXIT(8)
+            FDF_SWEEP_STEP(9) FDF_STEP_EXIT(9)
+            FDF_SWEEP_STEP(10) FDF_STEP_EXIT(10)
             FDF_SWEEP_STEP(11)
         }
         if constexpr (K >= 16) {
-            FDF_SWEEP_STEP(12)
-            FDF_SWEEP_STEP(13)
-            FDF_SWEEP_STEP(14)
+            FDF_STEP_EXIT(11)
+            FDF_SWEEP_STEP(12) FDF_STEP_EXIT(12)
+            FDF_SWEEP_STEP(13) FDF_STEP_EXIT(13)
+            FDF_SWEEP_STEP(14) FDF_STEP_EXIT(14)
             FDF_SWEEP_STEP(15)
         }
+#undef FDF_STEP_EXIT
     }
 #undef FDF_SWEEP_STEP
-#undef FDF_WIN_PUT
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
@@ -1341,7 +1270,6 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
     sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
     sh.seltab = reinterpret_cast<const uint32_t*>(smem_raw + L.seltab);
-    sh.win = smem_raw + L.win + wave * kWinBytes;
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;
@@ -1535,6 +1463,14 @@ void fast_sweep_kernel(BandParams P) {
         if (threadIdx.x == 0) *s_ticket = atomicAdd(P.ticket, 1u) - P.ticket_base;
         __syncthreads();
         task = *s_ticket;
+        // a ticket past the grid means the counter and the host's base disagree: touch no
+        // band's memory, report it (bit 2 of the error word; fdf_api.cpp take_lookback_error)
+        if (task >= P.ntasks) {
+            if (threadIdx.x == 0 && P.lookback_error)
+                __hip_atomic_fetch_or(P.lookback_error, 4u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
     } else {
         task = band_task(P);
     }

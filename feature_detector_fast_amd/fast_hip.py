@@ -350,15 +350,20 @@ class Lanes:
     def close(self):
         """Wait for every lane, release the borrowed tensors, destroy the lanes' contexts
         (lane 0 is the device's process-wide context and stays)."""
-        for i in range(len(self.ctxs)):
-            if self._held[i]:
-                self._held[i][-1][0].synchronize()
-                self._held[i].clear()
-        for ctx in self.ctxs[1:]:
-            ctx.close()
-        self.ctxs = self.ctxs[:1]
-        self._ext = self._ext[:1]
-        self._held = self._held[:1]
+        try:
+            for q in self._held:
+                if q:
+                    q[-1][0].synchronize()
+        finally:
+            # also after a device error: drop the borrows and the lanes' contexts (each
+            # context's destroy drains its own stream first)
+            for ctx in self.ctxs[1:]:
+                ctx.close()
+            for q in self._held:
+                q.clear()
+            self.ctxs = self.ctxs[:1]
+            self._ext = self._ext[:1]
+            self._held = self._held[:1]
 
 
 def detect_device_rgb(frames, config, out, offsets, stream=None, device=None):
