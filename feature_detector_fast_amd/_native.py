@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "fdf_detect_batch_multi", "fdf_fetch_last_multi", "fdf_ctx_workspace_bytes",
     "fdf_detect_device_rgb", "fdf_circle", "fdf_calculate_offsets", "fdf_score_rings",
     "fdf_score_rings_device", "fdf_ctx_set_band_rows", "fdf_ctx_set_upload_chunks",
-    "fdf_ctx_recoveries",
+    "fdf_ctx_recoveries", "fdf_ctx_test_skew_tickets",
 )
 
 
@@ -160,6 +160,8 @@ def load():
     lib.fdf_pipeline_collect.argtypes = [vp, u64, vp, vp, sz, vp, ctypes.POINTER(sz)]
     lib.fdf_ctx_workspace_bytes.restype = ctypes.c_int
     lib.fdf_ctx_workspace_bytes.argtypes = [vp, ctypes.POINTER(u64)]
+    lib.fdf_ctx_test_skew_tickets.restype = ctypes.c_int
+    lib.fdf_ctx_test_skew_tickets.argtypes = [vp, u32]
     lib.fdf_ctx_set_geometry.restype = ctypes.c_int
     lib.fdf_ctx_set_geometry.argtypes = [vp, u32]
     lib.fdf_ctx_set_band_rows.restype = ctypes.c_int

@@ -1212,6 +1212,13 @@ int fdf_ctx_recoveries(fdf_ctx* ctx, uint64_t* upload_fallbacks, uint64_t* lookb
     return FDF_OK;
 }
 
+int fdf_ctx_test_skew_tickets(fdf_ctx* ctx, uint32_t delta) {
+    if (!ctx) return FDF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->ticket_next += delta;
+    return FDF_OK;
+}
+
 int fdf_ctx_set_geometry(fdf_ctx* ctx, uint32_t min_tasks) {
     if (!ctx) return FDF_ERR_ARG;
     std::lock_guard<std::mutex> lock(ctx->mu);

@@ -140,6 +140,16 @@ int fdf_ctx_workspace_bytes(fdf_ctx* ctx, uint64_t* bytes);
  * fallback. */
 int fdf_ctx_recoveries(fdf_ctx* ctx, uint64_t* upload_fallbacks, uint64_t* lookback_recoveries);
 
+/* Test hook (no effect on results otherwise): moves the context's host-side count of the
+ * direct-output start tickets by `delta`, as if the device counter and the host had fallen
+ * out of step (after the context's first launch, which zeroes both).  The next direct-output
+ * launch then hands `delta` workgroups tickets past its
+ * grid; each one touches no band's memory and sets the context's device error, so that launch
+ * is reported: a host call returns FDF_ERR_DEVICE, an asynchronous fdf_detect_device reports
+ * it at the context's next device call, once, and the counter is re-zeroed (later calls are
+ * correct).  tests/test_gpu_api.py drives it. */
+int fdf_ctx_test_skew_tickets(fdf_ctx* ctx, uint32_t delta);
+
 /*
  * Replaces fast_simd::detector(img, config) -> Vec<Point> (src/fast_simd.rs:847).
  * Host image (row-major u8, `stride_bytes` >= width; GrayImage always has stride == width),

@@ -111,6 +111,71 @@ def test_device_then_host_call_without_sync():
         assert np.array_equal(out[o[f]:o[f + 1]].cpu().numpy().astype(np.uint32), want), f
 
 
+def test_ticket_out_of_step_is_reported_once():
+    """A direct-output launch whose start tickets run past its grid (the device counter and
+    the host's base out of step, forced with fdf_ctx_test_skew_tickets) touches no band
+    memory outside the grid (fdf_sweep_impl.h fast_sweep_kernel) and is reported: a host call
+    returns FDF_ERR_DEVICE; an asynchronous device call reports it at the context's next
+    device call, exactly once; both contexts are correct again afterwards (the counter is
+    re-zeroed).  Also the pending-error path of ADVICE r05: a host call in between that sees
+    the device call's error word first keeps it for the next device call."""
+    import torch
+
+    lib = _native.load()
+    img = workloads.s1_frame(2)
+    want = oracle.detect(img, 16, 9, 1)
+    cfg = Config(16, 9, NonMaximalSuppression.MaxThreshold)
+    ccfg = _native.FdfConfig(16, 9, 1)
+    c = _native.Context(0)
+    try:
+        out = np.zeros((len(want) + 16, 2), dtype=np.uint32)
+        n = ctypes.c_size_t(0)
+        # (a context's first launch zeroes the counter and the host count: skew after it)
+        rc = lib.fdf_detect(c.handle, img.ctypes.data, 1920, 1080, 1920, ctypes.byref(ccfg),
+                            out.ctypes.data, out.shape[0], ctypes.byref(n))
+        assert rc == _native.FDF_OK and np.array_equal(out[: n.value], want)
+        # host call: the skewed launch is an error of that call
+        _native.check(lib.fdf_ctx_test_skew_tickets(c.handle, 5))
+        rc = lib.fdf_detect(c.handle, img.ctypes.data, 1920, 1080, 1920, ctypes.byref(ccfg),
+                            out.ctypes.data, out.shape[0], ctypes.byref(n))
+        assert rc == _native.FDF_ERR_DEVICE
+        rc = lib.fdf_detect(c.handle, img.ctypes.data, 1920, 1080, 1920, ctypes.byref(ccfg),
+                            out.ctypes.data, out.shape[0], ctypes.byref(n))
+        assert rc == _native.FDF_OK and np.array_equal(out[: n.value], want)
+        # device calls: the skewed launch returns OK (asynchronous), the next device call
+        # reports it -- after a host call in between -- once
+        one = torch.from_numpy(img).cuda().unsqueeze(0).contiguous()
+        d_out = torch.empty((len(want) + 16, 2), dtype=torch.int32, device="cuda")
+        d_offs = torch.zeros(2, dtype=torch.int64, device="cuda")
+        _native.check(lib.fdf_ctx_test_skew_tickets(c.handle, 7))
+        fast_hip.detect_device(one, cfg, d_out, d_offs, ctx=c)
+        torch.cuda.synchronize()
+        rc = lib.fdf_detect(c.handle, img.ctypes.data, 1920, 1080, 1920, ctypes.byref(ccfg),
+                            out.ctypes.data, out.shape[0], ctypes.byref(n))
+        assert rc == _native.FDF_OK and np.array_equal(out[: n.value], want)
+        with pytest.raises(_native.FdfError):
+            fast_hip.detect_device(one, cfg, d_out, d_offs, ctx=c)
+        fast_hip.detect_device(one, cfg, d_out, d_offs, ctx=c)
+        torch.cuda.synchronize()
+        o = d_offs.cpu().numpy()
+        assert o[1] == len(want)
+        assert np.array_equal(d_out[: o[1]].cpu().numpy().astype(np.uint32), want)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("nframes", [1, 2, 3])
+def test_dense_frames_default_geometry(nframes):
+    """the one-round geometry a single frame or a few get by default (short
+    latency bands, direct output, 4x slots) on dense noise frames, where bands take the
+    bitmap-slot and NMS-spill paths: every mode equals the oracle."""
+    frames = [workloads.s3_frame(70 + i) for i in range(nframes)]
+    for nms in (0, 1, 2):
+        pts, offs = fast_hip.detector_batch(np.stack(frames), Config(8, 9, NonMaximalSuppression(nms)))
+        for f, img in enumerate(frames):
+            assert np.array_equal(pts[offs[f]:offs[f + 1]], oracle.detect(img, 8, 9, nms)), (nms, f)
+
+
 def test_geometry_override_same_result():
     img = workloads.s1_frame(6, 800, 600)
     cfg = Config(16, 9, NonMaximalSuppression.SumAbsolute)

@@ -39,7 +39,20 @@ exp_c5ab() {
   echo c5ab done
 }
 
+# Two full-test batches in flight per wave (FDF_BATCH_SLOTS=2: each evaluated 6 rows after its
+# issue instead of 3) against the product build: interleaved, 3 rounds, one stream.
+exp_slots_ab() {
+  O=gpurun_out/r6_slots_ab
+  mkdir -p $O
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_1080.txt 3 "maxt:0,off:0,sad:0" "" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_slots2.so
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_4k.txt 3 "sad:0" \
+      "--width 3840 --height 2160 --frames 128 --threshold 8 --count 12" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_slots2.so
+  echo slots_ab done
+}
+
 case "${1:-}" in
-  c5ab) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab}" >&2; exit 2 ;;
+  c5ab|slots_ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab}" >&2; exit 2 ;;
 esac
