@@ -33,9 +33,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixels/sec 1920x1080 t=16 n=9 (+NMS) at 1/2/4/8 GPUs; keypoints bit-exact"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
-# timed regions sample the kernel durations of every k-th launch, k = timing_every(steps):
-# at least 10 samples when the run has them (each timestamped dispatch costs ~10 us of queue
-# time, profiles/r03/l10_gap_*.json, so not every launch of a long run is timed)
+# launch-duration percentiles need at least this many samples (timed_steps samples the
+# launches' own durations in a region of their own: a timestamped dispatch costs queue time)
 MIN_TIMED = 10
 NMS_NAMES = {"off": 0, "maxt": 1, "sad": 2}
 
@@ -65,6 +64,9 @@ def parse_args(argv=None):
     p.add_argument("--copies", type=int, default=0,
                    help="input copies of the shard (0 = one per lane and >= 512 MiB in all; "
                         "1 = every lane reads the same copy, the rounds-1-4 protocol, for A/Bs)")
+    p.add_argument("--inline-timing", action="store_true",
+                   help="timestamp the timed region's own dispatches (the rounds-1-5 protocol, "
+                        "for A/Bs) instead of sampling launch durations in a region of their own")
     p.add_argument("--lanes", type=int, default=3,
                    help="launch lanes: step k runs on lane k %% L, each lane a context with its "
                         "own HIP stream and no dependency between lanes (fast_hip.Lanes)")
@@ -78,12 +80,6 @@ def parse_args(argv=None):
                         "single-frame GPU and CPU legs, as the reference's bench takes "
                         "INPUT_FILE (benches/benchmark.rs:6-7); the batch stays synthetic")
     return p.parse_args(argv)
-
-
-def timing_every(steps):
-    """Sampling interval of the kernel timing: every launch up to 2 * MIN_TIMED steps, then
-    the largest interval that still samples MIN_TIMED launches (at most every 5th)."""
-    return max(1, min(5, steps // MIN_TIMED))
 
 
 # torch.distributed's reductions run on this device ("cpu" under gloo when ranks share a GPU)
@@ -548,14 +544,16 @@ class Timed:
         self.copy_steps = copy_steps or {}
 
 
-def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle=0.0):
+def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle=0.0,
+                sample=True, inline=False):
     """W warm-up steps, then K timed steps between barriers + synchronizes; one step = one
     fdf_detect_device call over a batch, step k on lane k % L (fast_hip.Lanes: a context and
     its own HIP stream per lane, no dependency between lanes, so a call's detector runs beside
     the previous calls' last workgroups and compaction).  `settle` > 0: before the warm-up
     steps, the same launches back to back for that many seconds (untimed), so the timed steps
     run at the GPU's sustained clocks -- a cold GPU's launches speed up over the first
-    ~30 ms of load."""
+    ~30 ms of load.  `sample`: the launches' own durations (t.det, t.com) from
+    the same calls in a region of their own before the timed one."""
     import torch
 
     n = len(lanes)
@@ -580,11 +578,29 @@ def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle
     for k in range(warmup):
         call(k)
     torch.cuda.synchronize()
-    # HIP events the library's dispatches timestamp on each lane's stream (fdf_ctx_set_timing):
-    # every launch's own duration, sampled every timing_every-th call of a lane (each
-    # timestamped dispatch costs ~10 us of queue time: profiles/r03/l10_gap_*.json)
-    for ctx in lanes.ctxs:
-        ctx.set_timing(True, every=timing_every(max(1, steps // n)))
+    # the launches' own durations: HIP events the library's dispatches timestamp on each
+    # lane's stream (fdf_ctx_set_timing), sampled in a region of their own before the timed
+    # one -- a timestamped dispatch costs queue time (one stream: 0.4367 -> 0.4478 ms per
+    # 512-frame step, profiles/r03/l10_gap_*.json), so the timed region runs without them
+    det, com = [], []
+
+    def collect():
+        for ctx in lanes.ctxs:
+            d, c = ctx.timing_samples()
+            det.extend(d.tolist())
+            com.extend(c.tolist())
+            ctx.set_timing(False)
+
+    if sample and not inline:
+        for ctx in lanes.ctxs:
+            ctx.set_timing(True)
+        for k in range(steps):
+            call(k)
+        torch.cuda.synchronize()
+        collect()
+    elif sample:
+        for ctx in lanes.ctxs:
+            ctx.set_timing(True)
     start = torch.cuda.Event(enable_timing=True)
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
     barrier(world)
@@ -601,12 +617,8 @@ def timed_steps(fast_hip, lanes, bufs, copies, cfg, steps, warmup, world, settle
     barrier(world)
     elapsed = time.perf_counter() - t0
     span_ms = max(start.elapsed_time(e) for e in ends)
-    det, com = [], []
-    for ctx in lanes.ctxs:
-        d, c = ctx.timing_samples()
-        det.extend(d.tolist())
-        com.extend(c.tolist())
-        ctx.set_timing(False)
+    if sample and inline:
+        collect()
     copy_steps = {}
     for k in range(steps):
         copy_steps[k % len(copies)] = copy_steps.get(k % len(copies), 0) + 1
@@ -623,7 +635,8 @@ def roofline_of(t, alg_bytes, in_bytes, traffic):
         own duration covers the others' beside it), so the span is what a launch costs the
         GPU; with one lane it is each launch's duration plus its compaction and the gaps.
       launch_ms_avg: the mean of the launches' own HIP-event durations (the isolated
-        kernel's duration with one lane; with L lanes ~L launches share the GPU in it).
+        kernel's duration with one lane; with L lanes ~L launches share the GPU in it),
+        from the same calls in a sampling region before the timed one (timed_steps).
     Percentiles only from >= MIN_TIMED samples (fewer: the mean alone)."""
     per_launch = t.span_ms / t.steps
     launch = float(np.mean(t.det)) if len(t.det) else float("nan")
@@ -808,7 +821,7 @@ def main(argv=None):
     out, offs = bufs.out[0], bufs.offs[0]
 
     tm = timed_steps(fast_hip, lanes, bufs, copies, cfg, args.steps, args.warmup, world,
-                     settle=args.settle_seconds)
+                     settle=args.settle_seconds, inline=args.inline_timing)
     elapsed = reduce_max(tm.elapsed, world, device)
 
     # ---- whole-batch parity against the CPU checker (outside the timed region), on every
@@ -839,6 +852,9 @@ def main(argv=None):
     alg_bytes = in_bytes + 8 * total_kp + 4 * count
     cfg_key = f"{W}x{H}_b{count}_t{args.threshold}_n{args.count}_{args.nms}"
     roofline = roofline_of(tm, alg_bytes, in_bytes, load_traffic(cfg_key, len(lanes)))
+    roofline["launch_ms_source"] = ("the timed region's own dispatches, timestamped" if args.inline_timing
+                                    else "the same calls in a sampling region before the timed one "
+                                         "(the timed region's dispatches are not timestamped)")
 
     extras = {}
     cpu = None

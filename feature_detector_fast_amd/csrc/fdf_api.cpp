@@ -196,11 +196,21 @@ hipError_t note_done(fdf_ctx* ctx, hipStream_t stream) {
 // The device work of the last enqueue (whatever stream it ran on) has finished.
 void wait_done(fdf_ctx* ctx) {
     if (!ctx->done_valid) return;
-    if (record_done(ctx) != hipSuccess) {
-        (void)hipStreamSynchronize(ctx->done_stream);
-        return;
+    const hipError_t e = record_done(ctx) == hipSuccess ? hipEventSynchronize(ctx->done)
+                                                        : hipStreamSynchronize(ctx->done_stream);
+    if (e == hipSuccess) ctx->done_valid = false;    // nothing of the context is outstanding
+}
+
+// hipStreamSynchronize of the context's own stream; when the last enqueue ran there, nothing
+// of the context is outstanding afterwards (the next wait_done returns at once: a host call's
+// completion event is never recorded and waited on after the fact)
+hipError_t sync_own_stream(fdf_ctx* ctx) {
+    const hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess && ctx->done_valid && ctx->done_stream == ctx->stream) {
+        ctx->done_valid = false;
+        ctx->done_pending = false;
     }
-    (void)hipEventSynchronize(ctx->done);
+    return e;
 }
 
 // Grow a workspace buffer to `need` elements (+1/8 headroom).  The old buffer may still be
@@ -881,7 +891,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         if (!host_out)
             e = hipMemcpyAsync(offs, offs_dev, sizeof(uint64_t) * (n_frames + 1ull),
                                hipMemcpyDeviceToHost, ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = sync_own_stream(ctx);
         if (e == hipSuccess && host_out)
             std::memcpy(offs, ctx->h_offs, sizeof(uint64_t) * (n_frames + 1ull));
         return e;
@@ -929,7 +939,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             note_done(ctx, ctx->stream) != hipSuccess)
             return FDF_ERR_DEVICE;
         // the host reads h_out next: the compaction must be done
-        if (host_out && hipStreamSynchronize(ctx->stream) != hipSuccess) return FDF_ERR_DEVICE;
+        if (host_out && sync_own_stream(ctx) != hipSuccess) return FDF_ERR_DEVICE;
     }
     ctx->last.valid = true;
     ctx->last.host_out = host_out;
@@ -964,7 +974,7 @@ int settle_user_points(fdf_ctx* ctx) {
     c.kp_stats = nullptr;
     c.group_sums = nullptr;
     if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        sync_own_stream(ctx) != hipSuccess) {
         ctx->last.valid = false;
         return FDF_ERR_DEVICE;
     }
@@ -1001,14 +1011,14 @@ int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
                                hipMemcpyDeviceToHost, ctx->stream);
     }
     if (L.host_out) {
-        if (e == hipSuccess && out_scores) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess && out_scores) e = sync_own_stream(ctx);
         if (e == hipSuccess) std::memcpy(out, ctx->h_out, n * sizeof(fdf_point));
         return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(out, ctx->d_out, n * sizeof(fdf_point), hipMemcpyDeviceToHost,
                            ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = sync_own_stream(ctx);
     return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
 }
 
@@ -1064,7 +1074,7 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
         // the two-call pattern follows: keep the frame for fdf_fetch_last's scores
         if (hipMemcpyAsync(ctx->d_in, data, (size_t)w * h, hipMemcpyHostToDevice, ctx->stream) !=
                 hipSuccess ||
-            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            sync_own_stream(ctx) != hipSuccess)
             return FDF_ERR_DEVICE;
         ctx->last.in_place = false;
     }
@@ -1477,7 +1487,7 @@ int fdf_score_points(fdf_ctx* ctx, const uint8_t* data, uint32_t width, uint32_t
     if (e == hipSuccess)
         e = hipMemcpyAsync(out_scores, d_scores, n_points * sizeof(uint16_t), hipMemcpyDeviceToHost,
                            ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = sync_own_stream(ctx);
     return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
 }
 
@@ -1552,7 +1562,7 @@ int fdf_score_rings(fdf_ctx* ctx, const uint8_t* centers, const uint8_t* rings, 
     if (e == hipSuccess)
         e = hipMemcpyAsync(out_scores, d_scores, n_rings * sizeof(uint16_t), hipMemcpyDeviceToHost,
                            ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = sync_own_stream(ctx);
     return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
 }
 

@@ -11,13 +11,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
-@pytest.mark.parametrize("steps,every", [(1, 1), (10, 1), (19, 1), (20, 2), (50, 5), (500, 5)])
-def test_timing_every(steps, every):
-    assert bench.timing_every(steps) == every
-    # the driver's 20 steps sample 10 launches, the default 50 steps 10
-    assert steps // every >= min(steps, bench.MIN_TIMED)
-
-
 @pytest.mark.parametrize("local", [0, 1, 5, 7])
 def test_select_device_one_rank_per_gpu(local):
     """The driver's torchrun path: LOCAL_RANK r -> cuda:r over the default backend (RCCL);

@@ -52,7 +52,33 @@ exp_slots_ab() {
   echo slots_ab done
 }
 
+# The headline protocol with and without timestamps on the timed region's own dispatches
+# (--inline-timing: rounds 1-5), interleaved, 3 rounds each, no extras.
+exp_timing_ab() {
+  O=gpurun_out/r6_timing_ab
+  mkdir -p $O
+  : > $O/ab.jsonl
+  for r in 1 2 3; do
+    for mode in separate inline; do
+      extra=""; [ $mode = inline ] && extra="--inline-timing"
+      timeout -k 10 200 python3 bench.py --no-extras --no-parity --cpu-seconds 0 $extra > $O/run.json 2> $O/run.err
+      python3 -c "import json; d=json.load(open('$O/run.json')); r=d['roofline']; print(json.dumps({'round': $r, 'mode': '$mode', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms_avg': r['kernel_ms_avg'], 'launch_ms_avg': r['launch_ms_avg']}))" >> $O/ab.jsonl
+    done
+  done
+  cat $O/ab.jsonl
+}
+
+# fdf_detect end to end on one 1080p frame (pinned / pageable in and out), 3 rounds
+exp_host() {
+  O=gpurun_out/r6_host
+  mkdir -p $O
+  for r in 1 2 3; do
+    timeout -k 10 120 python3 tools/host_latency.py --iters 300 --modes off,maxt --mem pinned,pageable --chunks 0 >> $O/host.txt
+  done
+  cat $O/host.txt
+}
+
 case "${1:-}" in
-  c5ab|slots_ab) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host}" >&2; exit 2 ;;
 esac
