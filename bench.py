@@ -369,7 +369,9 @@ def config5_4k(fast_hip, Config, NonMaximalSuppression, workloads, lanes, device
     lanes1 = fast_hip.Lanes(1, device.index or 0)
     buf1 = LaneBufs.__new__(LaneBufs)
     buf1.out, buf1.offs = bufs.out[:1], bufs.offs[:1]
-    t1 = timed_steps(fast_hip, lanes1, buf1, copies, cfg, steps, warmup, 1)
+    # (the same sustained-clock settle as the lanes leg: without it this leg read 0.70-0.72 ms
+    # per launch against 0.641 settled, profiles/r06/t4_c5ab/)
+    t1 = timed_steps(fast_hip, lanes1, buf1, copies, cfg, steps, warmup, 1, settle=settle)
     parity["input_checksums"] = sums_before
     parity["inputs_unchanged"] = [int(c.sum(dtype=torch.int64)) for c in copies] == sums_before
     in_bytes = frames * W * H

@@ -798,8 +798,9 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         }
     }
     // frames that start in pinned host memory must lie inside one pinned mapping for the DMA
-    // copies below; a range that runs past it is packed into the pinned staging buffer first
-    if (!in_place && !chunked) {
+    // copies below (the chunked upload's too); a range that runs past it is packed into the
+    // pinned staging buffer first
+    if (!in_place) {
         const size_t span = (size_t)(n_frames - 1) * frame_stride + (size_t)(h - 1) * row_stride +
                             px * w;
         hipPointerAttribute_t a, z;
@@ -850,11 +851,17 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                 e = hipMemcpyAsync(ctx->d_flags + c, ctx->h_flags + c, sizeof(uint32_t),
                                    hipMemcpyHostToDevice, ctx->copy_stream);
             if (e != hipSuccess) {
-                // the runtime cannot do this upload: one copy before the launch, from now on
+                // the runtime cannot do this upload: this call takes one copy before the
+                // launch (counted; the caller's chunk setting stays)
                 (void)hipStreamSynchronize(ctx->copy_stream);
+                (void)hipGetLastError();
+                ++ctx->upload_fallbacks;
+                const uint32_t saved = ctx->chunks;
                 ctx->chunks = 1;
-                return run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb,
-                                offs, host_out);
+                rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb,
+                              offs, host_out, user_out, user_cap);
+                ctx->chunks = saved;
+                return rc;
             }
         }
     } else {
@@ -906,7 +913,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             const uint32_t saved = ctx->chunks;
             ctx->chunks = 1;
             rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs,
-                          host_out);
+                          host_out, user_out, user_cap);
             ctx->chunks = saved;
             return rc;
         }

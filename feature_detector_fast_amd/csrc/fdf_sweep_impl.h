@@ -209,6 +209,7 @@ struct SweepShared {
     uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
     const uint32_t* seltab;  // select_bit's table (SweepLayout::seltab)
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
+    uint8_t* shift;        // FDF_LDS_SHIFT: this lane's 16 bytes of the wave's row buffer
 };
 
 struct UnitCtx {
@@ -596,6 +597,23 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
     inflight[QL] = false;
 }
 
+#if FDF_LDS_SHIFT
+// A lane row shifted by `off` bytes (+3: the row's x + 3 bytes; -3: the previous lane's last 3
+// bytes, then the lane's first 13) through the wave's LDS row buffer: one 16-byte write, then
+// four 4-byte reads at unaligned addresses.  LDS operations of one wave execute in order; the
+// instruction-free wavefront fence keeps the compiler from forwarding the lane's own store.
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_shift(uint8_t* mine, const u32x4& v) {
+    *reinterpret_cast<u32x4*>(mine) = v;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    u32x4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const uint32_t*>(mine + OFF + 4 * k);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    return r;
+}
+#endif
+
 template <int NMS, int N, bool EXACT>
 __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     constexpr int LC = kLaneCols;
@@ -653,6 +671,13 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
     // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
     // their candidates masked: a branch around it costs the zeroing of `cand` on every step.
+#if FDF_LDS_SHIFT
+#define LDS_SHIFT_P3(v) lds_shift<3>(sh.shift, v)
+#define LDS_SHIFT_M3(v) lds_shift<-3>(sh.shift, v)
+#else
+#define LDS_SHIFT_P3(v) (v)
+#define LDS_SHIFT_M3(v) (v)
+#endif
 #define FDF_SWEEP_STEP(J)                                                                    \
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
@@ -665,15 +690,29 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
         {                                                                                    \
             RowV e;                                                                          \
-            _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
-            e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
+            if constexpr (kLdsShift >= 2) {                                                  \
+                e = LDS_SHIFT_P3(c);                                                         \
+            } else {                                                                         \
+                _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
+                e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                     \
+            }                                                                                \
             const RowFlags<LC> h = compare_rows<LC>(e, nc, lk);                              \
-            const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
+            RowV hbwv, hndwv;                                                                \
+            if constexpr (kLdsShift >= 1) {                                                  \
+                hbwv = LDS_SHIFT_M3(h.b);                                                    \
+                hndwv = LDS_SHIFT_M3(h.nd);                                                  \
+            } else {                                                                         \
+                const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
+                _Pragma("unroll") for (int m = 0; m < M; ++m) {                              \
+                    hbwv[m] = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);                     \
+                    hndwv[m] = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);                 \
+                }                                                                            \
+            }                                                                                \
             const RowFlags<LC>& vs = V[(J) & 3];                                             \
             const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
             _Pragma("unroll") for (int m = 0; m < M; ++m) {                                  \
-                const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);              \
-                const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);          \
+                const uint32_t hbw = hbwv[m];                                                \
+                const uint32_t hndw = hndwv[m];                                              \
                 const uint32_t bn = ~vn.nd[m], bs = vs.b[m], be = h.b[m], bw = ~hndw;        \
                 const uint32_t dn = ~vn.b[m], ds = vs.nd[m], de = h.nd[m], dw = ~hbw;        \
                 uint32_t br, nd;                                                             \
@@ -770,6 +809,8 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
 #undef FDF_STEP_EXIT
     }
 #undef FDF_SWEEP_STEP
+#undef LDS_SHIFT_P3
+#undef LDS_SHIFT_M3
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
@@ -1270,6 +1311,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
     sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
     sh.seltab = reinterpret_cast<const uint32_t*>(smem_raw + L.seltab);
+    sh.shift = smem_raw + L.shift + wave * kShiftBytes + 16u + 16u * lane;
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;

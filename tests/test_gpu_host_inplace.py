@@ -166,11 +166,14 @@ def test_in_place_other_pinned_kinds(kind):
             assert hip.hipHostUnregister(ptr) == 0
 
 
-def test_in_place_registered_range_shorter_than_frame():
+@pytest.mark.parametrize("chunks", [0, 4])
+def test_in_place_registered_range_shorter_than_frame(chunks):
     """a frame whose first bytes sit in a hipHostRegister'ed range that ends before
     the frame does is copied, not read in place (reading it in place would read past the
     registration over PCIe).  The frame's last byte must map to the same contiguous device
-    range as its first (fdf_api.cpp run_host)."""
+    range as its first (fdf_api.cpp run_host).  ADVICE r05: the overlapped chunked upload
+    (chunks = 4) stages such a frame as well, so no chunk copy is rejected and no fallback is
+    counted."""
     W, H = 1280, 720
     img = workloads.s1_frame(11, W, H)
     hip = _hip()
@@ -182,6 +185,7 @@ def test_in_place_registered_range_shorter_than_frame():
     assert hip.hipHostRegister(ctypes.c_void_p(base), ctypes.c_size_t(half), ctypes.c_uint(0)) == 0
     lib = _native.load()
     ctx = _native.Context(0)
+    ctx.set_upload_chunks(chunks)
     try:
         for nms in (0, 1, 2):
             rc, got, _ = _detect(lib, ctx, base, W, H, 16, 9, nms)

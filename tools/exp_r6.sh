@@ -78,7 +78,27 @@ exp_host() {
   cat $O/host.txt
 }
 
+# Lane-row byte shifts through LDS instead of v_alignbyte + DPP (FDF_LDS_SHIFT=1: the W flags;
+# 2: also the x + 3 row): whole-batch parity of each variant, then the interleaved A/B against
+# the product build (1080p three modes, 4K SAD), then VALU / LDS instruction counts.
+exp_lds_ab() {
+  O=gpurun_out/r6_lds_ab
+  mkdir -p $O
+  for v in lds1 lds2; do
+    FDF_LIB_PATH=build/libfdf_$v.so timeout -k 10 300 python3 -u -m pytest -q --timeout 200 --timeout-method thread \
+        tests/test_gpu_stress.py::test_config4_exact_batch tests/test_gpu_geometry.py::test_config5_batch_repeated \
+        tests/test_gpu_parity.py > $O/parity_$v.txt 2>&1 || { tail -20 $O/parity_$v.txt; exit 1; }
+    tail -1 $O/parity_$v.txt
+  done
+  timeout -k 10 500 bash tools/ab_interleave.sh $O/ab_1080.txt 3 "maxt:0,off:0,sad:0" "" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_lds1.so build/libfdf_lds2.so
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_4k.txt 3 "sad:0" \
+      "--width 3840 --height 2160 --frames 128 --threshold 8 --count 12" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_lds1.so build/libfdf_lds2.so
+  echo lds_ab done
+}
+
 case "${1:-}" in
-  c5ab|slots_ab|timing_ab|host) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host|lds_ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab}" >&2; exit 2 ;;
 esac
