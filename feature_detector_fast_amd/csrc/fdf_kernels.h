@@ -90,18 +90,8 @@ constexpr uint32_t kRankBlock = 4;            // bitmap words per rank-prefix bl
 static_assert(kScoreListCap * 2 <= 4 * kSweepPixelQ * 4, "ranked scores must fit the FIFO area");
 static_assert(kScoreListCap % 256 == 0, "the spill NMS pass holds the list 1/256 per thread");
 static_assert(kScoreListCap < 4096, "the LDS NMS pass keeps rank + 1 in a list entry's 12 score bits");
-// Byte shifts of a lane row through LDS instead of v_alignbyte + DPP (FDF_LDS_SHIFT, A/B
-// variant builds): 1 = the W flags (the horizontal flags of column x - 3, 8 alignbyte + 2 DPP
-// per sweep step), 2 = also the x + 3 row (4 alignbyte + 1 DPP).  Each wave writes a row of
-// 64 lanes x 16 bytes and reads it back 3 bytes off: kShiftBytes per wave (16-byte pads).
-#ifndef FDF_LDS_SHIFT
-#define FDF_LDS_SHIFT 0
-#endif
-constexpr int kLdsShift = FDF_LDS_SHIFT;
-constexpr uint32_t kShiftBytes = kLdsShift ? 1024u + 32u : 0u;
 struct SweepLayout {
     uint32_t pq, wave_bytes, stage, bitmap, slist, bprefix, rprefix, misc, total;
-    uint32_t shift;              // FDF_LDS_SHIFT: 4 per-wave row buffers of kShiftBytes
     uint32_t seltab;             // during the sweep: the 256-entry set-bit table (1 KB) in
                                  // the rank-prefix area, which NMS uses only after the sweep
     uint32_t nms_area_entries;   // u16 ranked scores that fit [pq, bprefix) after the sweep
@@ -125,8 +115,7 @@ __host__ __device__ inline SweepLayout make_sweep_layout(uint32_t R, uint32_t nw
     L.seltab = L.bprefix;
     const uint32_t prefix_end = L.rprefix + (nms ? align16(rows * 4) : 0u);
     L.misc = prefix_end > L.seltab + 1024u ? prefix_end : L.seltab + 1024u;
-    L.shift = L.misc + 64;
-    L.total = L.shift + 4 * kShiftBytes;
+    L.total = L.misc + 64;
     return L;
 }
 

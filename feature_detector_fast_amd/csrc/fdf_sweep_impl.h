@@ -73,6 +73,14 @@ constexpr int kWavesEU = FDF_SWEEP_TU_WAVES;
 #endif
 constexpr bool kExitInBlock = FDF_SWEEP_TU_EXIT != 0;
 constexpr int kPx = kRgb ? 3 : 1;
+// A/B variant (FDF_ROW_PLUS3 = D, off in the product): the x + 3 row of the horizontal
+// comparisons from its own 16-byte load at byte offset +3, issued D sweep steps ahead into a
+// ring of E_SLOTS registers, instead of 4 v_alignbyte + 1 DPP move per step.
+#ifndef FDF_ROW_PLUS3
+#define FDF_ROW_PLUS3 0
+#endif
+constexpr int kRowPlus3 = kRgb ? 0 : FDF_ROW_PLUS3;
+constexpr int kPlus3Slots = kRowPlus3 <= 2 ? 2 : 4;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -209,7 +217,6 @@ struct SweepShared {
     uint32_t* spill;       // NMS: entries past slist_cap, in the band's output slot (global)
     const uint32_t* seltab;  // select_bit's table (SweepLayout::seltab)
     uint32_t spill_cap;    // slot words (0 with slist_cap 0)
-    uint8_t* shift;        // FDF_LDS_SHIFT: this lane's 16 bytes of the wave's row buffer
 };
 
 struct UnitCtx {
@@ -597,23 +604,6 @@ __device__ __forceinline__ void flush_tests(const SweepShared& sh, UnitCtx& u,
     inflight[QL] = false;
 }
 
-#if FDF_LDS_SHIFT
-// A lane row shifted by `off` bytes (+3: the row's x + 3 bytes; -3: the previous lane's last 3
-// bytes, then the lane's first 13) through the wave's LDS row buffer: one 16-byte write, then
-// four 4-byte reads at unaligned addresses.  LDS operations of one wave execute in order; the
-// instruction-free wavefront fence keeps the compiler from forwarding the lane's own store.
-template <int OFF>
-__device__ __forceinline__ u32x4 lds_shift(uint8_t* mine, const u32x4& v) {
-    *reinterpret_cast<u32x4*>(mine) = v;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    u32x4 r;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const uint32_t*>(mine + OFF + 4 * k);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    return r;
-}
-#endif
-
 template <int NMS, int N, bool EXACT>
 __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, const LerpConsts& lk) {
     constexpr int LC = kLaneCols;
@@ -665,24 +655,21 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     for (int k = 0; k < 3; ++k) up[k] = load_row<LC, EXACT>(u.src, ys - 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
+    RowV Ep[kPlus3Slots];                              // FDF_ROW_PLUS3: rows yv .. at x + 3
+#pragma unroll
+    for (int k = 0; k < kRowPlus3; ++k) Ep[k % kPlus3Slots] = load_row<LC, EXACT>(u.src, ys + k, xb + 3);
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 #pragma unroll
     for (int k = 0; k < 3; ++k) V[k + 1] = compare_rows<LC>(Rw[k], ~up[k], lk);
     // Step J: next row load, comparisons, pre-filter of row yv, enqueue of its candidates.
     // Rows outside [p0, p1) (look-ahead and padding steps) run the pre-filter too and have
     // their candidates masked: a branch around it costs the zeroing of `cand` on every step.
-#if FDF_LDS_SHIFT
-#define LDS_SHIFT_P3(v) lds_shift<3>(sh.shift, v)
-#define LDS_SHIFT_M3(v) lds_shift<-3>(sh.shift, v)
-#else
-#define LDS_SHIFT_P3(v) (v)
-#define LDS_SHIFT_M3(v) (v)
-#endif
 #define FDF_SWEEP_STEP(J)                                                                    \
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
         RowV cand = (RowV)(0u);                                                              \
-        Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);                  \
+        if constexpr (!kRowPlus3)                                                            \
+            Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);              \
         const RowV s = Rw[((J) + 3) % K];                  /* row yv + 3 */                  \
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
@@ -690,29 +677,25 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
         {                                                                                    \
             RowV e;                                                                          \
-            if constexpr (kLdsShift >= 2) {                                                  \
-                e = LDS_SHIFT_P3(c);                                                         \
+            if constexpr (kRowPlus3) {                                                       \
+                e = Ep[(J) % kPlus3Slots];                                                   \
             } else {                                                                         \
                 _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
                 e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                     \
             }                                                                                \
             const RowFlags<LC> h = compare_rows<LC>(e, nc, lk);                              \
-            RowV hbwv, hndwv;                                                                \
-            if constexpr (kLdsShift >= 1) {                                                  \
-                hbwv = LDS_SHIFT_M3(h.b);                                                    \
-                hndwv = LDS_SHIFT_M3(h.nd);                                                  \
-            } else {                                                                         \
-                const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
-                _Pragma("unroll") for (int m = 0; m < M; ++m) {                              \
-                    hbwv[m] = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);                     \
-                    hndwv[m] = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);                 \
-                }                                                                            \
+            if constexpr (kRowPlus3) {                                                       \
+                /* the x + 3 row D steps ahead, then the ring row: a wait for the former */   \
+                /* never waits for a ring row issued after it */                             \
+                Ep[(J) % kPlus3Slots] = load_row<LC, EXACT>(u.src, yv + kRowPlus3, xb + 3);  \
+                Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);          \
             }                                                                                \
+            const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
             const RowFlags<LC>& vs = V[(J) & 3];                                             \
             const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
             _Pragma("unroll") for (int m = 0; m < M; ++m) {                                  \
-                const uint32_t hbw = hbwv[m];                                                \
-                const uint32_t hndw = hndwv[m];                                              \
+                const uint32_t hbw = alignbyte(h.b[m], m ? h.b[m - 1] : pb, 1);              \
+                const uint32_t hndw = alignbyte(h.nd[m], m ? h.nd[m - 1] : pnd, 1);          \
                 const uint32_t bn = ~vn.nd[m], bs = vs.b[m], be = h.b[m], bw = ~hndw;        \
                 const uint32_t dn = ~vn.b[m], ds = vs.nd[m], de = h.nd[m], dw = ~hbw;        \
                 uint32_t br, nd;                                                             \
@@ -809,8 +792,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
 #undef FDF_STEP_EXIT
     }
 #undef FDF_SWEEP_STEP
-#undef LDS_SHIFT_P3
-#undef LDS_SHIFT_M3
     flush_tests<NMS, N, LC>(sh, u, lk, inflight, batch);
 }
 
@@ -1311,7 +1292,6 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     sh.spill = reinterpret_cast<uint32_t*>(P.slots + (uint64_t)task * P.slot_bytes);
     sh.spill_cap = sh.slist_cap ? P.slot_bytes / 4 : 0u;
     sh.seltab = reinterpret_cast<const uint32_t*>(smem_raw + L.seltab);
-    sh.shift = smem_raw + L.shift + wave * kShiftBytes + 16u + 16u * lane;
 
     UnitCtx u;
     const uint8_t* img = P.frames + (uint64_t)frame * P.frame_stride;

@@ -98,7 +98,24 @@ exp_lds_ab() {
   echo lds_ab done
 }
 
+# The x + 3 row from its own unaligned 16-byte load, 2 steps ahead (FDF_ROW_PLUS3=2), against
+# the product build: parity, then the interleaved A/B (1080p three modes, 4K SAD).
+exp_p3_ab() {
+  O=gpurun_out/r6_p3_ab
+  mkdir -p $O
+  FDF_LIB_PATH=build/libfdf_p2.so timeout -k 10 300 python3 -u -m pytest -q --timeout 200 --timeout-method thread \
+      tests/test_gpu_stress.py::test_config4_exact_batch tests/test_gpu_geometry.py::test_config5_batch_repeated \
+      tests/test_gpu_parity.py > $O/parity_p2.txt 2>&1 || { tail -20 $O/parity_p2.txt; exit 1; }
+  tail -1 $O/parity_p2.txt
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_1080.txt 3 "maxt:0,off:0,sad:0" "" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_p2.so
+  timeout -k 10 300 bash tools/ab_interleave.sh $O/ab_4k.txt 3 "sad:0" \
+      "--width 3840 --height 2160 --frames 128 --threshold 8 --count 12" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_p2.so
+  echo p3_ab done
+}
+
 case "${1:-}" in
-  c5ab|slots_ab|timing_ab|host|lds_ab) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab}" >&2; exit 2 ;;
 esac
