@@ -73,14 +73,6 @@ constexpr int kWavesEU = FDF_SWEEP_TU_WAVES;
 #endif
 constexpr bool kExitInBlock = FDF_SWEEP_TU_EXIT != 0;
 constexpr int kPx = kRgb ? 3 : 1;
-// A/B variant (FDF_ROW_PLUS3 = D, off in the product): the x + 3 row of the horizontal
-// comparisons from its own 16-byte load at byte offset +3, issued D sweep steps ahead into a
-// ring of E_SLOTS registers, instead of 4 v_alignbyte + 1 DPP move per step.
-#ifndef FDF_ROW_PLUS3
-#define FDF_ROW_PLUS3 0
-#endif
-constexpr int kRowPlus3 = kRgb ? 0 : FDF_ROW_PLUS3;
-constexpr int kPlus3Slots = kRowPlus3 <= 2 ? 2 : 4;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -655,9 +647,6 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     for (int k = 0; k < 3; ++k) up[k] = load_row<LC, EXACT>(u.src, ys - 3 + k, xb);
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) Rw[k] = load_row<LC, EXACT>(u.src, ys + k, xb);
-    RowV Ep[kPlus3Slots];                              // FDF_ROW_PLUS3: rows yv .. at x + 3
-#pragma unroll
-    for (int k = 0; k < kRowPlus3; ++k) Ep[k % kPlus3Slots] = load_row<LC, EXACT>(u.src, ys + k, xb + 3);
     RowFlags<LC> V[4];                                 // vertical flags, slot (row-ys) & 3
 #pragma unroll
     for (int k = 0; k < 3; ++k) V[k + 1] = compare_rows<LC>(Rw[k], ~up[k], lk);
@@ -668,8 +657,7 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
     {                                                                                        \
         const int yv = ys + i0 + (J);                                                        \
         RowV cand = (RowV)(0u);                                                              \
-        if constexpr (!kRowPlus3)                                                            \
-            Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);              \
+        Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);                  \
         const RowV s = Rw[((J) + 3) % K];                  /* row yv + 3 */                  \
         const RowV c = Rw[(J) % K];                        /* row yv */                      \
         const RowV nc = ~c;                                                                  \
@@ -677,19 +665,9 @@ __device__ __forceinline__ void sweep_unit(const SweepShared& sh, UnitCtx& u, co
         const bool live = yv >= p0 && yv < p1 && !(ablation_flags(u.flags) & kFlagNoLoad);                  \
         {                                                                                    \
             RowV e;                                                                          \
-            if constexpr (kRowPlus3) {                                                       \
-                e = Ep[(J) % kPlus3Slots];                                                   \
-            } else {                                                                         \
-                _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
-                e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                     \
-            }                                                                                \
+            _Pragma("unroll") for (int m = 0; m + 1 < M; ++m) e[m] = alignbyte(c[m + 1], c[m], 3); \
+            e[M - 1] = alignbyte(from_next_lane(c[0]), c[M - 1], 3);                         \
             const RowFlags<LC> h = compare_rows<LC>(e, nc, lk);                              \
-            if constexpr (kRowPlus3) {                                                       \
-                /* the x + 3 row D steps ahead, then the ring row: a wait for the former */   \
-                /* never waits for a ring row issued after it */                             \
-                Ep[(J) % kPlus3Slots] = load_row<LC, EXACT>(u.src, yv + kRowPlus3, xb + 3);  \
-                Rw[((J) + K - 1) % K] = load_row<LC, EXACT>(u.src, yv + K - 1, xb);          \
-            }                                                                                \
             const uint32_t pb = from_prev_lane(h.b[M - 1]), pnd = from_prev_lane(h.nd[M - 1]); \
             const RowFlags<LC>& vs = V[(J) & 3];                                             \
             const RowFlags<LC>& vn = V[((J) + 1) & 3];                                       \
