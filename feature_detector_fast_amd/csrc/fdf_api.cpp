@@ -32,8 +32,6 @@ struct LastResult {
     bool rgb = false;              // frames in d_rgb (RGB8); scores need their luma in d_in
     bool in_place = false;         // the frame was read in place from pinned host memory: not
                                    // in d_in, so the result has no scores (fdf_fetch_last)
-    bool in_user = false;          // the points went straight into the caller's pinned buffer
-                                   // (not h_out: fdf_fetch_last compacts them again)
     // fdf_detect_batch_multi: the call's generation (0: not a multi-context result) and this
     // context's shard of it, checked by fdf_fetch_last_multi
     uint64_t multi_gen = 0;
@@ -708,7 +706,7 @@ int check_host_args(const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t
 // with image 0.24.6's to_luma8 before detection (src/main.rs:58).
 int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, uint32_t h,
              size_t row_stride, size_t frame_stride, const fdf_config* cfg, bool rgb,
-             uint64_t* offs, bool host_out, uint2* user_out = nullptr, size_t user_cap = 0) {
+             uint64_t* offs, bool host_out) {
     ctx->last = LastResult{};          // invalid, and not a shard of a multi-context call
     const size_t frame_bytes = (size_t)w * h;
     const size_t max_points = (size_t)(w - 6) * (h - 6) * n_frames;
@@ -728,10 +726,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         out_dev = ctx->hd_out;
         offs_dev = ctx->hd_offs;
         out_cap = &ctx->h_out_points;
-        if (user_out) {                // the caller's pinned buffer, written by the kernels
-            out_dev = user_out;
-            out_cap = &user_cap;
-        }
     } else {
         if ((rc = ensure(ctx, &ctx->d_out, &ctx->out_points, guess, ctx->stream))) return rc;
         if ((rc = ensure(ctx, &ctx->d_offsets, &ctx->offsets_n, n_frames + 1ull, ctx->stream)))
@@ -859,7 +853,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                 const uint32_t saved = ctx->chunks;
                 ctx->chunks = 1;
                 rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb,
-                              offs, host_out, user_out, user_cap);
+                              offs, host_out);
                 ctx->chunks = saved;
                 return rc;
             }
@@ -913,7 +907,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             const uint32_t saved = ctx->chunks;
             ctx->chunks = 1;
             rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs,
-                          host_out, user_out, user_cap);
+                          host_out);
             ctx->chunks = saved;
             return rc;
         }
@@ -957,34 +951,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     ctx->last.cfg = *cfg;
     ctx->last.rgb = false;          // the luma frames are in d_in
     ctx->last.in_place = in_place != nullptr;   // ... or were read in place (not in d_in)
-    ctx->last.in_user = user_out && total <= user_cap;
-    return FDF_OK;
-}
-
-// A host result whose points went straight into the caller's pinned buffer (LastResult::
-// in_user) exists only there: compact it again from the band slots into h_out (lock held).
-// Called before anything reads it back (fdf_fetch_last) and before a device call reuses the
-// slots and replaces last_compact.
-int settle_user_points(fdf_ctx* ctx) {
-    if (!ctx->last.valid || !ctx->last.in_user) return FDF_OK;
-    ctx->last.in_user = false;
-    if (ctx->last.total == 0) return FDF_OK;
-    int rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points,
-                         (size_t)ctx->last.total, ctx->stream);
-    if (rc) {
-        ctx->last.valid = false;
-        return rc;
-    }
-    fdfk::CompactParams c = ctx->last_compact;
-    c.out = ctx->hd_out;
-    c.cap = ctx->h_out_points;
-    c.kp_stats = nullptr;
-    c.group_sums = nullptr;
-    if (fdfk::launch_compact(c, ctx->stream) != hipSuccess ||
-        sync_own_stream(ctx) != hipSuccess) {
-        ctx->last.valid = false;
-        return FDF_ERR_DEVICE;
-    }
     return FDF_OK;
 }
 
@@ -992,7 +958,6 @@ int settle_user_points(fdf_ctx* ctx) {
 // `out_scores` is given, to the host.
 int copy_out(fdf_ctx* ctx, fdf_point* out, uint16_t* out_scores, size_t n) {
     if (!n) return FDF_OK;
-    if (int rc = settle_user_points(ctx)) return rc;
     const LastResult& L = ctx->last;
     if (out_scores && L.in_place) return FDF_ERR_ARG;
     hipError_t e = hipSuccess;
@@ -1057,24 +1022,10 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
         offs = local.data();
     }
     // unscored calls take the host-mapped output (no copy back); the scored ones keep the
-    // points on the device for the score kernel.  A caller's output buffer in pinned host
-    // memory (all `cap` points in one device-mapped range) is written by the kernels
-    // themselves, with no copy from h_out after the call.
-    uint2* user_out = nullptr;
-    if (!scored && cap) {
-        hipPointerAttribute_t a, z;
-        if (hipPointerGetAttributes(&a, out) == hipSuccess && a.type == hipMemoryTypeHost &&
-            a.devicePointer) {
-            const uint8_t* last = reinterpret_cast<const uint8_t*>(out) + cap * sizeof(fdf_point) - 1;
-            if (hipPointerGetAttributes(&z, last) == hipSuccess && z.type == hipMemoryTypeHost &&
-                static_cast<const uint8_t*>(z.devicePointer) ==
-                    static_cast<const uint8_t*>(a.devicePointer) + (cap * sizeof(fdf_point) - 1))
-                user_out = static_cast<uint2*>(a.devicePointer);
-        }
-        (void)hipGetLastError();       // pageable memory (or a range past the pinning): no error
-    }
-    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored,
-                  user_out, cap);
+    // points on the device for the score kernel.  (Points written straight into a caller's
+    // pinned output buffer, round 5 and again in round 6, came with an asynchronous device
+    // error in a later test in 3 of 5 full GPU-suite runs: DESIGN.md §7.7.)
+    rc = run_host(ctx, data, n_frames, w, h, row_stride, frame_stride, cfg, rgb, offs, !scored);
     if (rc) return rc;
     const uint64_t total = offs[n_frames];
     if (total > cap && ctx->last.in_place) {
@@ -1085,10 +1036,8 @@ int detect_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w
             return FDF_ERR_DEVICE;
         ctx->last.in_place = false;
     }
-    if (!ctx->last.in_user) {
-        rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
-        if (rc) return rc;
-    }
+    rc = copy_out(ctx, out, scored ? out_scores : nullptr, (size_t)std::min<uint64_t>(total, cap));
+    if (rc) return rc;
     *n_out = (size_t)total;
     return total > cap ? FDF_ERR_CAPACITY : FDF_OK;
 }
@@ -1413,8 +1362,6 @@ int fdf_detect_device(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames,
                    ? FDF_OK
                    : FDF_ERR_DEVICE;
     }
-    // the slots and last_compact are about to be reused
-    if (int rs = settle_user_points(ctx)) return rs;
     return enqueue(ctx, d_frames, n_frames, width, height,
                    n_frames > 1 ? frame_stride_bytes : (uint64_t)width * height, cfg,
                    reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s);
@@ -1451,8 +1398,6 @@ int fdf_detect_device_rgb(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_fram
                    ? FDF_OK
                    : FDF_ERR_DEVICE;
     }
-    // the slots and last_compact are about to be reused
-    if (int rs = settle_user_points(ctx)) return rs;
     return enqueue(ctx, d_frames, n_frames, width, height, n_frames > 1 ? frame_stride_bytes : fb,
                    cfg, reinterpret_cast<uint2*>(d_out), cap, d_frame_offsets, s, true);
 }

@@ -195,52 +195,3 @@ def test_in_place_registered_range_shorter_than_frame(chunks):
     finally:
         ctx.close()
         assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
-
-
-@pytest.mark.parametrize("nms", [0, 1])
-def test_pinned_output_buffer(nms):
-    """A caller's output buffer in pinned memory is written by the kernels directly (no copy
-    from the context's staging after the call): the list equals the oracle; fdf_fetch_last
-    afterwards rebuilds the same list from the band slots; with cap below the total the first
-    cap points are there and FDF_ERR_CAPACITY + fdf_fetch_last give the rest."""
-    import torch
-
-    W, H = 1920, 1080
-    img = workloads.s1_frame(5)
-    want = oracle.detect(img, 16, 9, nms)
-    buf = _pinned(W * H)
-    buf.numpy()[:] = img.reshape(-1)
-    lib = _native.load()
-    ctx = _native.Context(0)
-    cfg = _native.FdfConfig(16, 9, nms)
-    try:
-        for cap in (len(want) + 100, len(want), len(want) // 2):
-            pout = torch.zeros((cap, 2), dtype=torch.int32).pin_memory()
-            got = ctypes.c_size_t(0)
-            rc = lib.fdf_detect(ctx.handle, ctypes.c_void_p(buf.data_ptr()), W, H, W,
-                                ctypes.byref(cfg), ctypes.c_void_p(pout.data_ptr()), cap,
-                                ctypes.byref(got))
-            assert got.value == len(want)
-            k = min(cap, len(want))
-            assert rc == (_native.FDF_OK if cap >= len(want) else _native.FDF_ERR_CAPACITY)
-            assert np.array_equal(pout.numpy()[:k].astype(np.uint32), want[:k]), cap
-            full = np.zeros((len(want), 2), dtype=np.uint32)
-            _native.check(lib.fdf_fetch_last(ctx.handle, full.ctypes.data, None, len(want),
-                                             ctypes.byref(got)), "fdf_fetch_last")
-            assert np.array_equal(full, want), cap
-        # a batch of two frames into one pinned buffer
-        two = np.stack([img, workloads.s1_frame(6)])
-        wants = [oracle.detect(f, 16, 9, nms) for f in two]
-        n = sum(len(x) for x in wants)
-        pin2 = _pinned(two.size)
-        pin2.numpy()[:] = two.reshape(-1)
-        pout = torch.zeros((n + 8, 2), dtype=torch.int32).pin_memory()
-        offs = np.zeros(3, dtype=np.uint64)
-        got = ctypes.c_size_t(0)
-        _native.check(lib.fdf_detect_batch(ctx.handle, ctypes.c_void_p(pin2.data_ptr()), 2, W, H,
-                                           W * H, ctypes.byref(cfg), ctypes.c_void_p(pout.data_ptr()),
-                                           n + 8, offs.ctypes.data, ctypes.byref(got)), "batch")
-        assert got.value == n and list(offs) == [0, len(wants[0]), n]
-        assert np.array_equal(pout.numpy()[:n].astype(np.uint32), np.concatenate(wants))
-    finally:
-        ctx.close()
