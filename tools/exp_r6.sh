@@ -115,7 +115,28 @@ exp_p3_ab() {
   echo p3_ab done
 }
 
+# Final-tree instruction counts per detector launch (one lane, serialised dispatches): the
+# round-5 t25 passes (tools/exp_r5.sh t25_pmcv) into gpurun_out/r6_pmcv.
+exp_pmcv() {
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  O=gpurun_out/r6_pmcv
+  mkdir -p $O
+  SHORT="--steps 6 --warmup 1 --settle-seconds 0 --cpu-seconds 0 --no-extras --no-parity --lanes 1"
+  run() {
+    local tag=$1; shift
+    timeout -k 10 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES \
+        --output-format csv -d "$O/$tag" -o p -- python3 bench.py $SHORT "$@" > "$O/$tag.json" 2> "$O/$tag.log"
+    python3 tools/pmc_summary.py "$O/$tag" > "$O/${tag}_summary.json"
+    rm -rf "$O/$tag"
+  }
+  run maxt --nms maxt
+  run off --nms off
+  run sad --nms sad
+  run 4k --width 3840 --height 2160 --frames 128 --threshold 8 --count 12 --nms sad
+  cat $O/*_summary.json
+}
+
 case "${1:-}" in
-  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv}" >&2; exit 2 ;;
 esac
