@@ -8,6 +8,8 @@ equals the CPU oracle (oracle/fast_oracle.c, pinned to the reference's goldens; 
 contract is src/fast_simd.rs:307-330).  The two-call pattern keeps the frame for
 fdf_fetch_last's scores; a result that fit asks for fdf_detect_scored instead."""
 import ctypes
+import json
+import os
 
 import numpy as np
 import pytest
@@ -121,33 +123,22 @@ def _hip():
 
     _native.load()
     hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_NOW)
-    for fn in ("hipHostMalloc", "hipHostRegister", "hipHostFree", "hipHostUnregister"):
+    for fn in ("hipHostMalloc", "hipHostFree"):
         getattr(hip, fn).restype = ctypes.c_int
     return hip
 
 
-@pytest.mark.parametrize("kind", ["coherent", "registered"])
-def test_in_place_other_pinned_kinds(kind):
-    """Fine-grained (coherent) pinned memory is copied, not read in place; memory registered
-    with hipHostRegister is read in place.  Either way the lists equal the oracle, across
-    frames written into the same buffer."""
+def test_in_place_coherent_pinned_is_copied():
+    """Fine-grained (coherent) pinned memory is copied, not read in place; the lists equal the
+    oracle across frames written into the same buffer."""
     W, H = 1280, 720
     frames = [workloads.s1_frame(3, W, H), workloads.s3_frame(7)[:H, :W].copy(),
               workloads.s1_frame(40, W, H)]
     hip = _hip()
     ptr = ctypes.c_void_p()
-    keep = None
-    if kind == "coherent":
-        assert hip.hipHostMalloc(ctypes.byref(ptr), ctypes.c_size_t(W * H),
-                                 ctypes.c_uint(0x40000000)) == 0
-        view = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
-    else:
-        keep = np.zeros(W * H + 4096, dtype=np.uint8)
-        base = keep.ctypes.data + (-keep.ctypes.data) % 4096   # page-aligned start
-        view = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
-        assert hip.hipHostRegister(ctypes.c_void_p(base), ctypes.c_size_t(W * H),
-                                   ctypes.c_uint(0)) == 0
-        ptr = ctypes.c_void_p(base)
+    assert hip.hipHostMalloc(ctypes.byref(ptr), ctypes.c_size_t(W * H),
+                             ctypes.c_uint(0x40000000)) == 0
+    view = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
     lib = _native.load()
     ctx = _native.Context(0)
     try:
@@ -157,41 +148,26 @@ def test_in_place_other_pinned_kinds(kind):
                 view[:] = f.reshape(-1)
                 rc, got, _ = _detect(lib, ctx, ptr.value, W, H, 16, 9, nms)
                 _native.check(rc, "fdf_detect")
-                assert np.array_equal(got, oracle.detect(f, 16, 9, nms)), (kind, rep, i, nms)
+                assert np.array_equal(got, oracle.detect(f, 16, 9, nms)), (rep, i, nms)
     finally:
         ctx.close()
-        if kind == "coherent":
-            assert hip.hipHostFree(ptr) == 0
-        else:
-            assert hip.hipHostUnregister(ptr) == 0
+        assert hip.hipHostFree(ptr) == 0
 
 
-@pytest.mark.parametrize("chunks", [0, 4])
-def test_in_place_registered_range_shorter_than_frame(chunks):
-    """a frame whose first bytes sit in a hipHostRegister'ed range that ends before
-    the frame does is copied, not read in place (reading it in place would read past the
-    registration over PCIe).  The frame's last byte must map to the same contiguous device
-    range as its first (fdf_api.cpp run_host).  ADVICE r05: the overlapped chunked upload
-    (chunks = 4) stages such a frame as well, so no chunk copy is rejected and no fallback is
-    counted."""
-    W, H = 1280, 720
-    img = workloads.s1_frame(11, W, H)
-    hip = _hip()
-    keep = np.zeros(W * H + 4096, dtype=np.uint8)
-    base = keep.ctypes.data + (-keep.ctypes.data) % 4096
-    view = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (W * H,))
-    view[:] = img.reshape(-1)
-    half = (W * H // 2) & ~4095                       # whole pages, half the frame
-    assert hip.hipHostRegister(ctypes.c_void_p(base), ctypes.c_size_t(half), ctypes.c_uint(0)) == 0
-    lib = _native.load()
-    ctx = _native.Context(0)
-    ctx.set_upload_chunks(chunks)
-    try:
-        for nms in (0, 1, 2):
-            rc, got, _ = _detect(lib, ctx, base, W, H, 16, 9, nms)
-            _native.check(rc, "fdf_detect")
-            assert np.array_equal(got, oracle.detect(img, 16, 9, nms)), nms
-        assert ctx.recoveries() == (0, 0)
-    finally:
-        ctx.close()
-        assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
+@pytest.mark.parametrize("case", ["registered", "shorter0", "shorter4"])
+def test_in_place_host_registered_ranges(case):
+    """Memory the caller registered with hipHostRegister: a whole frame is read in place
+    ("registered"); a registered range shorter than the frame is copied, not read past its
+    end, by the single copy and by the chunked upload ("shorter0" / "shorter4"; ADVICE r04,
+    r05).  The cases register and unregister ranges of their own numpy memory, so they run in
+    a child process (tests/_host_register_cases.py): that memory is never
+    handed back to this session's allocator and its later pageable copies."""
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_host_register_cases.py")
+    r = subprocess.run([sys.executable, "-u", script, case], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["ok"] and res["case"] == case and res["calls"] >= 3, res
