@@ -283,8 +283,11 @@ class Lanes:
         if n < 1:
             raise ValueError("at least one lane")
         self.device = int(device)
-        self.ctxs = [context(self.device)]
-        for _ in range(n - 1):
+        # every lane a context of its own, the process-wide context(device) included: no
+        # state of other callers' calls (workspace sizes, ticket counters, completion stream)
+        # reaches a lane, and close() destroys them all
+        self.ctxs = []
+        for _ in range(n):
             ctx = _native.Context(self.device)
             ctx.lock = threading.Lock()
             self.ctxs.append(ctx)
@@ -348,8 +351,7 @@ class Lanes:
             cur.wait_stream(self.stream(i))
 
     def close(self):
-        """Wait for every lane, release the borrowed tensors, destroy the lanes' contexts
-        (lane 0 is the device's process-wide context and stays)."""
+        """Wait for every lane, release the borrowed tensors, destroy the lanes' contexts."""
         try:
             for q in self._held:
                 if q:
@@ -357,13 +359,13 @@ class Lanes:
         finally:
             # also after a device error: drop the borrows and the lanes' contexts (each
             # context's destroy drains its own stream first)
-            for ctx in self.ctxs[1:]:
+            for ctx in self.ctxs:
                 ctx.close()
             for q in self._held:
                 q.clear()
-            self.ctxs = self.ctxs[:1]
-            self._ext = self._ext[:1]
-            self._held = self._held[:1]
+            self.ctxs = []
+            self._ext = []
+            self._held = []
 
 
 def detect_device_rgb(frames, config, out, offsets, stream=None, device=None):
