@@ -1482,9 +1482,11 @@ int fdf_score_rings_device(fdf_ctx* ctx, const uint8_t* d_centers, const uint8_t
     if (n_rings == 0) return FDF_OK;
     if (!d_centers || !d_rings || !d_scores || ((uintptr_t)d_rings & 15u)) return FDF_ERR_ARG;
     DeviceGuard guard(ctx->device);
+    // NULL = the HIP null stream, as for every device-pointer call (torch's default stream is
+    // NULL: the context's own stream would not be ordered with it)
     const hipError_t e = fdfk::launch_score_rings(d_centers, d_rings, (uint32_t)n_rings, cfg->nms,
                                                   cfg->threshold, ring_count(cfg), d_scores,
-                                                  stream ? (hipStream_t)stream : ctx->stream);
+                                                  reinterpret_cast<hipStream_t>(stream));
     return e == hipSuccess ? FDF_OK : FDF_ERR_DEVICE;
 }
 

@@ -287,7 +287,8 @@ void fdf_calculate_offsets(uint32_t width, int32_t offsets[16]);
  * Runs on the GPU through the detector's own score functions (see fdf_kernels.hip), for any
  * ring.  fdf_score_rings: host in/out, synchronous; invalidates fdf_fetch_last's result.
  * fdf_score_rings_device: device pointers, d_rings 16-byte aligned, asynchronous on
- * `stream` (NULL = the context's stream).
+ * `stream` (NULL = the HIP null stream, as for fdf_detect_device; round 6 -- NULL meant the
+ * context's stream before, which is not ordered with work on the null stream).
  */
 int fdf_score_rings(fdf_ctx* ctx, const uint8_t* centers, const uint8_t* rings, size_t n_rings,
                     const fdf_config* cfg, uint16_t* out_scores);

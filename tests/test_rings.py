@@ -160,3 +160,25 @@ def test_score_rings_device_argument_checks():
         fast_hip.score_rings_device(c, r.to(torch.int16), s, SAD)
     with pytest.raises(ValueError, match="CUDA"):
         fast_hip.score_rings_device(c, r, s, SAD)
+
+
+@pytest.mark.gpu
+def test_score_rings_device_runs_in_stream_order():
+    """Round 6: score_rings_device on torch's default stream (handle NULL) runs in that stream's
+    order -- after the work enqueued before it, before the copy back.  The default stream first
+    spins ~20 ms and then fills ``out`` with -1: a launch on any other stream would score first
+    and have its scores overwritten by the fill."""
+    import torch
+    rng = np.random.default_rng(29)
+    c, r = planted_rings(rng, 50_000, 9)
+    dc = torch.from_numpy(c).cuda()
+    dr = torch.from_numpy(r).cuda()
+    out = torch.zeros(c.size, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    assert torch.cuda.current_stream().cuda_stream == 0       # the HIP null stream
+    for score, t, n, mode in ((SAD, 30, 9, 2), (MAXT, 0, 9, 1)):
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(50_000_000)
+        out.fill_(-1)
+        fast_hip.score_rings_device(dc, dr, out, score, threshold=t, consecutive=n)
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), oracle.score_rings(c, r, mode, t, n))
