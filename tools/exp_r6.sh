@@ -136,7 +136,28 @@ exp_pmcv() {
   cat $O/*_summary.json
 }
 
+# fdf_detect returning on the launch's completion word (the product) against the runtime's
+# completion (FDF_NO_DONE_FLAG build): the host-call tests on the product build, then
+# interleaved end-to-end host latency, 3 rounds, pinned and pageable frames.
+exp_host_word_ab() {
+  O=gpurun_out/r6_host_word_ab
+  mkdir -p $O
+  timeout -k 10 300 python3 -u -m pytest -q --timeout 200 --timeout-method thread \
+      tests/test_gpu_host_inplace.py tests/test_gpu_api.py tests/test_gpu_parity.py \
+      > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+  tail -1 $O/tests.txt
+  : > $O/host.txt
+  for r in 1 2 3; do
+    for lib in feature_detector_fast_amd/libfdf.so build/libfdf_nodone.so; do
+      echo "== round $r $lib" >> $O/host.txt
+      FDF_LIB_PATH=$lib timeout -k 10 120 python3 tools/host_latency.py --iters 300 \
+          --modes off,maxt --mem pinned,pageable --chunks 0 >> $O/host.txt
+    done
+  done
+  cat $O/host.txt
+}
+
 case "${1:-}" in
-  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab}" >&2; exit 2 ;;
 esac

@@ -14,6 +14,12 @@ __global__ void touch(uint32_t* p) {
     if (threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1;
 }
 
+// writes `seq` to a host-mapped word with a system-scope release (a vector store)
+__global__ void touch_flag(uint32_t* flag, uint32_t seq) {
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // each thread reads 16-byte words i, i + stride, ... of the buffer and folds them into one
 // word per thread (written, so the loads are not dead)
 __global__ void read_all(const uint4* __restrict__ p, size_t n16, uint32_t* sink) {
@@ -57,6 +63,34 @@ int main() {
             if (i >= 100) t.push_back(now_us() - t0);
         }
         report(mode == 0 ? "launch+hipStreamSynchronize" : "launch+hipStreamQuery_poll", t);
+    }
+    {
+        // round 6: the host waits for a word the kernel writes to pinned host memory instead
+        // of the runtime's completion (the stream is drained afterwards, untimed)
+        uint32_t* hf = nullptr;
+        uint32_t* df = nullptr;
+        if (hipHostMalloc(&hf, 64, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&df), hf, 0) != hipSuccess)
+            return 1;
+        *hf = 0;
+        std::vector<double> t, tsync;
+        for (int i = 0; i < iters + 100; ++i) {
+            const uint32_t seq = (uint32_t)i + 1;
+            const double t0 = now_us();
+            touch_flag<<<1, 64, 0, s>>>(df, seq);
+            while (__atomic_load_n(reinterpret_cast<volatile uint32_t*>(hf), __ATOMIC_ACQUIRE) != seq)
+                __builtin_ia32_pause();
+            const double t1 = now_us();
+            (void)hipStreamSynchronize(s);
+            const double t2 = now_us();
+            if (i >= 100) {
+                t.push_back(t1 - t0);
+                tsync.push_back(t2 - t0);
+            }
+        }
+        report("launch+host_flag_seen", t);
+        report("launch+host_flag_then_sync", tsync);
+        (void)hipHostFree(hf);
     }
     {
         std::vector<double> t;
