@@ -139,10 +139,12 @@ struct fdf_ctx {
 };
 
 constexpr size_t kMaxTimedCalls = 4096;
-// Host-call output (points, offsets, the completion word): fine-grained pinned host memory,
-// not cached in the GPU's L2, so a band's completed stores are in host memory (BandParams::
-// done_flag).  FDF_NO_DONE_FLAG builds (A/B only) wait for the runtime's completion instead.
-constexpr unsigned kHostOutFlags = hipHostMallocMapped | hipHostMallocCoherent;
+// Host-call output (points, offsets, the completion word): pinned, device-mapped host memory.
+// A launch armed with the completion word writes into it with system-scope stores (through
+// the L2: fine-grained host memory is cached there like any other on gfx950, measured), so a
+// band's completed stores are in host memory (BandParams::done_flag).  FDF_NO_DONE_FLAG
+// builds (A/B only) wait for the runtime's completion instead.
+constexpr unsigned kHostOutFlags = hipHostMallocMapped;
 #ifdef FDF_NO_DONE_FLAG
 constexpr bool kDoneFlag = false;
 #else
