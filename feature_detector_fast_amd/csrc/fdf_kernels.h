@@ -221,8 +221,9 @@ struct BandParams {
     // `dev_error` (device word).  With `done_flag` (fdf_detect: a word of fine-grained host
     // memory) the last workgroup to finish writes done_seq there -- bit 31 set if the launch
     // had an error -- so the host sees the launch done without the runtime's completion
-    // (DESIGN.md §7.5).  Such a launch writes its points and offsets with system-scope stores
-    // (through the L2 to host memory), so their completed stores are what the host reads.
+    // (DESIGN.md §7.5).  Each workgroup of such a launch writes its XCD's L2 back
+    // (system-scope release) before it counts itself finished, so the points and offsets
+    // are in host memory when the word is.
     uint32_t* finish;
     uint32_t* dev_error;
     uint32_t* done_flag;

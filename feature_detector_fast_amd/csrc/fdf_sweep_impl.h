@@ -1191,17 +1191,6 @@ __device__ __forceinline__ uint32_t band_task(const BandParams& P) {
     return task;
 }
 
-// Direct output into a host call's output (BandParams::done_flag armed): system-scope stores,
-// which write through the GPU's L2 to host memory, so that once the band's stores have
-// completed the host can read them (the host call returns on the completion word without the
-// runtime's end-of-launch cache writeback).  Otherwise plain stores.
-__device__ __forceinline__ void put_offset(const BandParams& P, uint32_t i, uint64_t v) {
-    if (P.done_flag)
-        __hip_atomic_store(&P.frame_offsets[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else
-        P.frame_offsets[i] = v;
-}
-
 // Sweeps band `task`, runs its NMS and writes its slot; returns the band's keypoint count.
 template <int NMS, int N>
 __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* smem_raw, uint32_t task,
@@ -1222,8 +1211,8 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
     uint32_t* wave_sum = reinterpret_cast<uint32_t*>(smem_raw + L.misc);
     if (P.threshold >= 255) {                                        // no pixel can pass
         if (P.direct && tid == 0) {
-            if (band == 0) put_offset(P, frame, 0);
-            if (task == P.ntasks - 1) put_offset(P, frame + 1, 0);
+            if (band == 0) P.frame_offsets[frame] = 0;
+            if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = 0;
         }
         return 0;
     }
@@ -1420,10 +1409,9 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
         direct = dbase != kLbNoBase;                  // timed out: the slot only
     }
     if (direct && tid == 0) {
-        if (band == 0) put_offset(P, frame, dbase);
-        if (task == P.ntasks - 1) put_offset(P, frame + 1, dbase + total);
+        if (band == 0) P.frame_offsets[frame] = dbase;
+        if (task == P.ntasks - 1) P.frame_offsets[frame + 1] = dbase + total;
     }
-    const bool through = P.done_flag != nullptr;     // wave-uniform
     if (listed || direct) {
         uint2* pts = reinterpret_cast<uint2*>(slot);
         uint32_t o = before;
@@ -1448,14 +1436,7 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
                 }
                 const uint2 pt = make_uint2(xb + bit, y0 + r);
                 if (listed) pts[idx] = pt;
-                if (direct && dbase + idx < P.cap) {
-                    if (through)
-                        __hip_atomic_store(reinterpret_cast<uint64_t*>(P.out + dbase + idx),
-                                           ((uint64_t)pt.y << 32) | pt.x, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    else
-                        P.out[dbase + idx] = pt;
-                }
+                if (direct && dbase + idx < P.cap) P.out[dbase + idx] = pt;
                 ++idx;
             }
         }
@@ -1507,12 +1488,14 @@ void fast_sweep_kernel(BandParams P) {
         if (P.group_sums) atomicAdd(&P.group_sums[task / P.tasks_per_group], total);
     }
     if (P.direct && P.finish) {
-        // every wave's stores (points, offsets, slot, count, error words) have completed --
-        // a host call's points and offsets through to host memory (put_offset) -- before the
-        // workgroup counts itself finished; the last one to finish tells the host
+        // every wave's stores (points, offsets, slot, count, error words) have completed
+        // before the workgroup counts itself finished; the last one to finish tells the host.
+        // A host call's launch first writes its XCD's L2 back to memory (system-scope release):
+        // the points and offsets in host memory are cached there like any other lines
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
+            if (P.done_flag) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             const uint32_t fin = __hip_atomic_fetch_add(P.finish, 1u, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT) - P.ticket_base;
             if (P.done_flag && fin == P.ntasks - 1) {
