@@ -930,7 +930,10 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
-    ctx->want_done_flag = kDoneFlag && host_out;
+    // (frames read in place only: a pageable or copied frame's next call starts with a
+    // runtime copy on this stream, which then waits for the launch's completion anyway --
+    // measured 2-4 us slower per call that way, profiles/r06/t17_host_word_ab/)
+    ctx->want_done_flag = kDoneFlag && host_out && in_place != nullptr;
     rc = enqueue(ctx, in_place ? in_place : ctx->d_in, n_frames, w, h, frame_bytes, cfg,
                  out_dev, *out_cap, offs_dev, ctx->stream, false, up, in_place != nullptr);
     const uint32_t armed = rc ? 0u : ctx->armed_seq;

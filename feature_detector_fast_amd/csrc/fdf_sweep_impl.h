@@ -1499,6 +1499,7 @@ void fast_sweep_kernel(BandParams P) {
             const uint32_t fin = __hip_atomic_fetch_add(P.finish, 1u, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT) - P.ticket_base;
             if (P.done_flag && fin == P.ntasks - 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // after every count
                 const uint32_t err = P.dev_error ? __hip_atomic_exchange(P.dev_error, 0u,
                                                                          __ATOMIC_RELAXED,
                                                                          __HIP_MEMORY_SCOPE_AGENT)
