@@ -103,14 +103,6 @@ struct fdf_ctx {
     // record waits until something needs it (another stream's call, a host wait), so a
     // stream of back-to-back calls enqueues one packet per call, not two
     bool done_pending = false;
-    // fdf_detect's completion word (fine-grained pinned host memory, BandParams::done_flag):
-    // the last workgroup of a direct-output launch writes the call's sequence number there
-    uint32_t* h_done = nullptr;
-    uint32_t* hd_done = nullptr;
-    uint32_t done_seq = 0;
-    bool want_done_flag = false;   // run_host: arm the word for the next enqueue
-    uint32_t armed_seq = 0;        // enqueue: the sequence number it armed (0: none)
-    bool flag_return = false;      // the last call was a host call that returned on the word
     // the last enqueue's compaction, relaunched when the host output has to grow
     fdfk::CompactParams last_compact{};
     LastResult last;
@@ -139,17 +131,6 @@ struct fdf_ctx {
 };
 
 constexpr size_t kMaxTimedCalls = 4096;
-// Host-call output (points, offsets, the completion word): pinned, device-mapped host memory.
-// A launch armed with the completion word writes into it with system-scope stores (through
-// the L2: fine-grained host memory is cached there like any other on gfx950, measured), so a
-// band's completed stores are in host memory (BandParams::done_flag).  FDF_NO_DONE_FLAG
-// builds (A/B only) wait for the runtime's completion instead.
-constexpr unsigned kHostOutFlags = hipHostMallocMapped;
-#ifdef FDF_NO_DONE_FLAG
-constexpr bool kDoneFlag = false;
-#else
-constexpr bool kDoneFlag = true;
-#endif
 constexpr uint64_t kDefaultMinTasks = 1024;   // 4 workgroups on each of 256 CUs
 constexpr uint32_t kMaxBandRows = 256;        // fdf_ctx_set_band_rows: the automatic path's range
 constexpr uint32_t kMaxChunks = 16;           // overlapped upload: chunks at most
@@ -254,8 +235,7 @@ int ensure(fdf_ctx* ctx, T** buf, size_t* have, size_t need, hipStream_t stream)
 // Grow a pinned, device-mapped host buffer to `need` elements (+1/8 headroom); *dev is its
 // device address.  Like ensure(), everything the context enqueued is drained first.
 template <typename T>
-int ensure_host(fdf_ctx* ctx, T** buf, T** dev, size_t* have, size_t need, hipStream_t stream,
-                unsigned flags = hipHostMallocMapped) {
+int ensure_host(fdf_ctx* ctx, T** buf, T** dev, size_t* have, size_t need, hipStream_t stream) {
     if (*have >= need) return FDF_OK;
     if (*buf) {
         wait_done(ctx);
@@ -267,7 +247,7 @@ int ensure_host(fdf_ctx* ctx, T** buf, T** dev, size_t* have, size_t need, hipSt
     const size_t n = need + need / 8;
     void* hp = nullptr;
     void* dp = nullptr;
-    if (hipHostMalloc(&hp, n * sizeof(T), flags) != hipSuccess) return FDF_ERR_ALLOC;
+    if (hipHostMalloc(&hp, n * sizeof(T), hipHostMallocMapped) != hipSuccess) return FDF_ERR_ALLOC;
     if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
         (void)hipHostFree(hp);
         return FDF_ERR_ALLOC;
@@ -610,12 +590,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
     p.chunk_flags = up.flags;
     p.chunk_rows = up.rows;
     p.chunk_epoch = up.epoch;
-    p.finish = nullptr;
-    p.dev_error = nullptr;
-    p.done_flag = nullptr;
-    p.done_seq = 0;
-    ctx->armed_seq = 0;
-    ctx->flag_return = false;
     if (direct) {
         // a (re)allocated buffer is zeroed: recycled device memory can hold descriptors of
         // another context's launches.  Launch tags are unique in the process as well.
@@ -628,17 +602,6 @@ int enqueue(fdf_ctx* ctx, const uint8_t* d_frames, uint32_t n_frames, uint32_t w
         uint32_t e = ++g_launch_epoch;
         if (e == 0) e = ++g_launch_epoch;                          // 0 = a zeroed descriptor
         p.epoch = e;
-        // every direct launch counts its finished workgroups (in step with the tickets); a
-        // host call's launch also reports its end in the completion word (run_host)
-        p.finish = ctx->d_sums + 2 * fdfk::kMaxGroupSums + 3;
-        if (ctx->want_done_flag && ctx->hd_done) {
-            uint32_t q = ++ctx->done_seq & 0x7fffffffu;
-            if (q == 0) q = ++ctx->done_seq & 0x7fffffffu;
-            p.dev_error = ctx->d_sums + 2 * fdfk::kMaxGroupSums;
-            p.done_flag = ctx->hd_done;
-            p.done_seq = q;
-            ctx->armed_seq = q;
-        }
     }
 #ifdef FDF_DEBUG_BUILD
     if (std::getenv("FDF_STAMPS")) {
@@ -755,24 +718,11 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     uint64_t* offs_dev;
     size_t* out_cap;
     if (host_out) {
-        if ((rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points, guess, ctx->stream,
-                              kHostOutFlags)))
+        if ((rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points, guess, ctx->stream)))
             return rc;
         if ((rc = ensure_host(ctx, &ctx->h_offs, &ctx->hd_offs, &ctx->h_offs_n, n_frames + 1ull,
-                              ctx->stream, kHostOutFlags)))
+                              ctx->stream)))
             return rc;
-        if (kDoneFlag && !ctx->h_done) {
-            void* hp = nullptr;
-            void* dp = nullptr;
-            if (hipHostMalloc(&hp, 64, kHostOutFlags) == hipSuccess &&
-                hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
-                std::memset(hp, 0, 64);
-                ctx->h_done = static_cast<uint32_t*>(hp);
-                ctx->hd_done = static_cast<uint32_t*>(dp);
-            } else if (hp) {
-                (void)hipHostFree(hp);   // no word: this context takes the runtime's completion
-            }
-        }
         out_dev = ctx->hd_out;
         offs_dev = ctx->hd_offs;
         out_cap = &ctx->h_out_points;
@@ -791,6 +741,12 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             return rc;
         stage = ctx->d_rgb;
     }
+    // the host frames are read by the copies below: nothing else may still read d_in (nor
+    // the host output, which the host reads after this call)
+    wait_done(ctx);
+    // an error an earlier asynchronous fdf_detect_device left in the error word belongs to
+    // that call: keep it for the next device call, so this call's own check sees only its own
+    if (take_lookback_error(ctx)) ctx->pending_device_error = true;
     // one grey frame of >= kChunkMinBytes: upload it in row chunks on the copy stream while
     // the detector runs, each band waiting for the chunk of its last row (the H2D of a 1080p
     // frame is ~45 us, the detector ~20 us: DESIGN.md §7.5)
@@ -804,15 +760,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
                                                     kMaxChunks);
     const bool chunked = host_out && !rgb && n_frames == 1 && frame_bytes >= kChunkMinBytes &&
                          nchunks_eff > 1 && ctx->h_stats && ensure_chunk_flags(ctx) == FDF_OK;
-    // the host frames are read by the copies below: nothing else may still read d_in (nor
-    // the host output, which the host reads after this call) -- except right after a host
-    // call that returned on its completion word: its launch, finishing on the context's own
-    // stream, is ahead of these copies there (not of the chunked upload's copy stream)
-    if (chunked || !ctx->flag_return) wait_done(ctx);
-    ctx->flag_return = false;
-    // an error an earlier asynchronous fdf_detect_device left in the error word belongs to
-    // that call: keep it for the next device call, so this call's own check sees only its own
-    if (take_lookback_error(ctx)) ctx->pending_device_error = true;
     // one packed grey frame in pinned (page-locked, non-coherent) host memory, unscored: the
     // detector reads it in place over PCIe, with no copy before the launch -- its row stream
     // is the upload (1080p max-t 72-75 vs 82-83 us end to end).  Host writes
@@ -930,15 +877,8 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     if (rgb && fdfk::launch_rgb_to_luma(ctx->d_rgb, n_frames, (uint32_t)frame_bytes,
                                         3 * frame_bytes, ctx->d_in, ctx->stream) != hipSuccess)
         return FDF_ERR_DEVICE;
-    // (frames read in place only: a pageable or copied frame's next call starts with a
-    // runtime copy on this stream, which then waits for the launch's completion anyway --
-    // measured 2-4 us slower per call that way, profiles/r06/t17_host_word_ab/)
-    ctx->want_done_flag = kDoneFlag && host_out && in_place != nullptr;
     rc = enqueue(ctx, in_place ? in_place : ctx->d_in, n_frames, w, h, frame_bytes, cfg,
                  out_dev, *out_cap, offs_dev, ctx->stream, false, up, in_place != nullptr);
-    const uint32_t armed = rc ? 0u : ctx->armed_seq;
-    ctx->want_done_flag = false;
-    ctx->armed_seq = 0;
     if (chunked) {
         // the copies end before the detector does (it waits for the last one), but a failed
         // launch or a timed-out wait would leave them running: drain them before any return
@@ -957,33 +897,8 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
             std::memcpy(offs, ctx->h_offs, sizeof(uint64_t) * (n_frames + 1ull));
         return e;
     };
-    // A direct-output launch armed with the completion word: its last workgroup writes the
-    // call's number there once every band's points and offsets are in host memory (bit 31: a
-    // wait in the launch ran out), ~5 us before the runtime reports the launch complete
-    // (profiles/r06/t16_sync_latency.txt).  If the stream finishes, or fails, without the
-    // word, the call takes the runtime's completion as before.
-    bool via_word = false;
-    if (armed) {
-        const volatile uint32_t* word = ctx->h_done;
-        for (uint32_t polls = 1;; ++polls) {
-            const uint32_t v = __atomic_load_n(word, __ATOMIC_ACQUIRE);
-            if ((v & 0x7fffffffu) == armed) {
-                via_word = (v & 0x80000000u) == 0;
-                break;
-            }
-            if ((polls & 255u) == 0 && hipStreamQuery(ctx->stream) != hipErrorNotReady) {
-                via_word = __atomic_load_n(word, __ATOMIC_ACQUIRE) == armed;
-                break;
-            }
-            __builtin_ia32_pause();
-        }
-    }
-    if (via_word) {
-        std::memcpy(offs, ctx->h_offs, sizeof(uint64_t) * (n_frames + 1ull));
-    } else if (fetch_offsets() != hipSuccess) {
-        return FDF_ERR_DEVICE;
-    }
-    if (const uint32_t err = via_word ? 0u : take_lookback_error(ctx)) {
+    if (fetch_offsets() != hipSuccess) return FDF_ERR_DEVICE;
+    if (const uint32_t err = take_lookback_error(ctx)) {
         if (err & 4u) return FDF_ERR_DEVICE;   // a band never ran: nothing to rebuild from
         if (err & 2u) {
             // a band's wait for its upload chunk ran out (the copies are drained now): detect
@@ -1012,7 +927,7 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
         fdfk::CompactParams c = ctx->last_compact;
         if (host_out) {
             if ((rc = ensure_host(ctx, &ctx->h_out, &ctx->hd_out, &ctx->h_out_points, (size_t)total,
-                                  ctx->stream, kHostOutFlags)))
+                                  ctx->stream)))
                 return rc;
             c.out = ctx->hd_out;
         } else {
@@ -1036,7 +951,6 @@ int run_host(fdf_ctx* ctx, const uint8_t* data, uint32_t n_frames, uint32_t w, u
     ctx->last.cfg = *cfg;
     ctx->last.rgb = false;          // the luma frames are in d_in
     ctx->last.in_place = in_place != nullptr;   // ... or were read in place (not in d_in)
-    ctx->flag_return = via_word && total <= *out_cap;
     return FDF_OK;
 }
 
@@ -1230,7 +1144,6 @@ void fdf_ctx_destroy(fdf_ctx* ctx) {
         for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
         if (ctx->done) (void)hipEventDestroy(ctx->done);
         if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
-        if (ctx->h_done) (void)hipHostFree(ctx->h_done);
         (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;

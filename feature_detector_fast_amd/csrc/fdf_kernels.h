@@ -215,19 +215,6 @@ struct BandParams {
     const uint32_t* chunk_flags;
     uint32_t chunk_rows;
     uint32_t chunk_epoch;
-    // Direct output: every workgroup counts itself finished in `finish` (a device counter that
-    // runs in step with `ticket`: each launch adds exactly ntasks to both), after all its
-    // stores have completed.  The look-back and chunk waits also OR their error bits into
-    // `dev_error` (device word).  With `done_flag` (fdf_detect: a word of fine-grained host
-    // memory) the last workgroup to finish writes done_seq there -- bit 31 set if the launch
-    // had an error -- so the host sees the launch done without the runtime's completion
-    // (DESIGN.md §7.5).  Each workgroup of such a launch writes its XCD's L2 back
-    // (system-scope release) before it counts itself finished, so the points and offsets
-    // are in host memory when the word is.
-    uint32_t* finish;
-    uint32_t* dev_error;
-    uint32_t* done_flag;
-    uint32_t done_seq;
 };
 constexpr uint64_t kLbAggregate = 1ull << 30;   // value = the band's own keypoint count
 constexpr uint64_t kLbPrefix = 1ull << 31;      // value = keypoints of bands 0 .. this one

@@ -1141,9 +1141,6 @@ __device__ uint64_t band_lookback(const BandParams& P, uint32_t task, uint32_t t
                 if (P.lookback_error)
                     __hip_atomic_fetch_or(P.lookback_error, 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                if (P.dev_error)
-                    __hip_atomic_fetch_or(P.dev_error, 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
                 *s_base = kLbNoBase;
             } else {
                 __hip_atomic_store(&P.lookback[task], ep | kLbPrefix | ((excl + total) & kLbValue),
@@ -1251,9 +1248,6 @@ __device__ __forceinline__ uint32_t sweep_band(const BandParams& P, uint8_t* sme
                 if (P.lookback_error && lane == 0)
                     __hip_atomic_fetch_or(P.lookback_error, 2u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                if (P.dev_error && lane == 0)
-                    __hip_atomic_fetch_or(P.dev_error, 2u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -1486,28 +1480,6 @@ void fast_sweep_kernel(BandParams P) {
     if (tid == 0) {
         P.counts[task] = total;
         if (P.group_sums) atomicAdd(&P.group_sums[task / P.tasks_per_group], total);
-    }
-    if (P.direct && P.finish) {
-        // every wave's stores (points, offsets, slot, count, error words) have completed
-        // before the workgroup counts itself finished; the last one to finish tells the host.
-        // A host call's launch first writes its XCD's L2 back to memory (system-scope release):
-        // the points and offsets in host memory are cached there like any other lines
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            if (P.done_flag) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            const uint32_t fin = __hip_atomic_fetch_add(P.finish, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT) - P.ticket_base;
-            if (P.done_flag && fin == P.ntasks - 1) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // after every count
-                const uint32_t err = P.dev_error ? __hip_atomic_exchange(P.dev_error, 0u,
-                                                                         __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                                 : 0u;
-                __hip_atomic_store(P.done_flag, P.done_seq | (err ? 0x80000000u : 0u),
-                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
     }
     if constexpr (kDebugBuild) {
         if (P.stamps) {
