@@ -138,7 +138,9 @@ exp_pmcv() {
 
 # fdf_detect returning on the launch's completion word (the product) against the runtime's
 # completion (FDF_NO_DONE_FLAG build): the host-call tests on the product build, then
-# interleaved end-to-end host latency, 3 rounds, pinned and pageable frames.
+# interleaved end-to-end host latency, 3 rounds, pinned and pageable frames.  Measured and not
+# kept: the sources it needs are the completion-word commits in git history
+# (profiles/r06/t17_host_word_ab/README.txt).
 exp_host_word_ab() {
   O=gpurun_out/r6_host_word_ab
   mkdir -p $O
