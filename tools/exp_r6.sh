@@ -159,7 +159,26 @@ exp_host_word_ab() {
   cat $O/host.txt
 }
 
+# Full-test issue cadence (FDF_ISSUE: a batch every 2 / 3 / 4 rows) at 4K t=8 n=12 SAD, where a
+# wave queues ~35 candidates per row (FIFO overflow -> synchronous batches), and at 1080p:
+# parity of the 4K batch on each variant, then interleaved A/B (3 rounds, one stream).
+exp_issue_ab() {
+  O=gpurun_out/r6_issue_ab
+  mkdir -p $O
+  for v in issue2 issue4; do
+    FDF_LIB_PATH=build/libfdf_$v.so timeout -k 10 200 python3 -u -m pytest -q --timeout 150 --timeout-method thread \
+        tests/test_gpu_geometry.py::test_config5_batch_repeated > $O/parity_$v.txt 2>&1 || { tail -20 $O/parity_$v.txt; exit 1; }
+    tail -1 $O/parity_$v.txt
+  done
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_4k.txt 3 "sad:0" \
+      "--width 3840 --height 2160 --frames 128 --threshold 8 --count 12" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_issue2.so build/libfdf_issue4.so
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_1080.txt 3 "maxt:0,sad:0" "" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_issue2.so build/libfdf_issue4.so
+  echo issue_ab done
+}
+
 case "${1:-}" in
-  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab|issue_ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab|issue_ab}" >&2; exit 2 ;;
 esac
