@@ -178,7 +178,28 @@ exp_issue_ab() {
   echo issue_ab done
 }
 
+# Candidate FIFO of 512 / 1024 entries per wave (an FDF_PIXEL_Q macro for kSweepPixelQ, 256;
+# measured and not kept, the macro is not in the product header): at 4K t=8
+# the 256-entry FIFO overflows and its overflow path tests batches synchronously.  Parity on
+# the config-5 batch and test_gpu_parity.py, then interleaved A/B at 4K and 1080p.
+exp_fifo_ab() {
+  O=gpurun_out/r6_fifo_ab
+  mkdir -p $O
+  for v in q512 q1024; do
+    FDF_LIB_PATH=build/libfdf_$v.so timeout -k 10 300 python3 -u -m pytest -q --timeout 200 --timeout-method thread \
+        tests/test_gpu_geometry.py::test_config5_batch_repeated tests/test_gpu_stress.py::test_config4_exact_batch \
+        tests/test_gpu_parity.py > $O/parity_$v.txt 2>&1 || { tail -20 $O/parity_$v.txt; exit 1; }
+    tail -1 $O/parity_$v.txt
+  done
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_4k.txt 3 "sad:0" \
+      "--width 3840 --height 2160 --frames 128 --threshold 8 --count 12" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_q512.so build/libfdf_q1024.so
+  timeout -k 10 400 bash tools/ab_interleave.sh $O/ab_1080.txt 3 "maxt:0,off:0,sad:0" "" \
+      feature_detector_fast_amd/libfdf.so build/libfdf_q512.so build/libfdf_q1024.so
+  echo fifo_ab done
+}
+
 case "${1:-}" in
-  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab|issue_ab) "exp_$1" ;;
-  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab|issue_ab}" >&2; exit 2 ;;
+  c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab|issue_ab|fifo_ab) "exp_$1" ;;
+  *) echo "usage: $0 {c5ab|slots_ab|timing_ab|host|lds_ab|p3_ab|pmcv|host_word_ab|issue_ab|fifo_ab}" >&2; exit 2 ;;
 esac
