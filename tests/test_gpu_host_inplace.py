@@ -171,3 +171,4 @@ def test_in_place_host_registered_ranges(case):
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["ok"] and res["case"] == case and res["calls"] >= 3, res
+
